@@ -1,0 +1,166 @@
+/*
+ * trt/abi.h — the C-ABI drop-in for the reference's compute-shader hot path.
+ *
+ * The reference's "operator boundary" is a Vulkan descriptor set with seven bindings
+ * (main.cpp:1218-1274) plus one vkCmdDispatch per frame (main.cpp:2108-2131).  Each
+ * entry point below replaces one piece of that boundary:
+ *
+ *   trt_create / trt_destroy   <- device + pipeline setup (main.cpp:547-725, 1394-1427)
+ *                                 and teardown (main.cpp:440-526)
+ *   trt_upload_scene           <- createShaderStorageBuffers() (main.cpp:1494-1647:
+ *                                 binding 5 triangles, binding 6 models), createUniformBuffers()
+ *                                 (main.cpp:1650-1664, binding 0) and the background texture
+ *                                 upload + sampler (main.cpp:928-1111, binding 4)
+ *   trt_update_ubo             <- updateUniformBuffer() (main.cpp:2165-2179)
+ *   trt_render                 <- recordComputeCommandBuffer() + vkQueueSubmit
+ *                                 (main.cpp:2108-2131, 2181-2205); binding 1 (rayIn) is
+ *                                 trt_params.rays_in, binding 2 (rayOut.resultColor) is
+ *                                 out_rgba32f, binding 3 (storage image) is out_rgba8.
+ *
+ * Conventions: every function returns 0 (TRT_OK) or a negative TRT_ERR_* code and never
+ * throws; trt_last_error() returns the message of the last failure on that context.  The
+ * caller owns every host array (copied during the call).  The context owns its device
+ * buffers until trt_destroy().  Calls on one context are serialised by the caller; use one
+ * context per GPU.
+ */
+#ifndef TRT_ABI_H
+#define TRT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "scene_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRT_ABI_VERSION 1
+
+/* status codes */
+#define TRT_OK 0
+#define TRT_ERR_INVALID (-1) /* bad argument (null pointer, size, depth, band) */
+#define TRT_ERR_HIP (-2)     /* HIP runtime failure (no device, launch, copy) */
+#define TRT_ERR_NOSCENE (-3) /* trt_render before trt_upload_scene */
+#define TRT_ERR_OOM (-4)     /* host or device allocation failed */
+#define TRT_ERR_IO (-5)      /* file could not be read or parsed */
+
+/* trt_params.flags */
+#define TRT_FLAG_SPHERES (1u << 0)     /* draw_sphere, shader.comp:83 (false in the shipped shader) */
+#define TRT_FLAG_FLOOR (1u << 1)       /* draw_floor, shader.comp:84 */
+#define TRT_FLAG_CHECKER (1u << 2)     /* checker floor colour, shader.comp:312 (commented out upstream) */
+#define TRT_FLAG_ENVMAP (1u << 3)      /* miss -> envmap, shader.comp:455-456; else BACKGROUND_COLOR :77 */
+#define TRT_FLAG_ROW_QUIRK (1u << 4)   /* the pix++ off-by-one of main.cpp:1501-1502 */
+#define TRT_FLAG_DEVICE_PTRS (1u << 5) /* out_rgba8 / out_rgba32f / rays_in are device pointers */
+#define TRT_FLAG_COUNT (1u << 6)       /* fill trt_stats ray counters */
+#define TRT_FLAG_TIMING (1u << 7)      /* fill trt_stats.kernel_ms (waits for the frame) */
+
+/* The shipped shader: floor on, spheres off, envmap background, host ray quirk. */
+#define TRT_FLAGS_REFERENCE (TRT_FLAG_FLOOR | TRT_FLAG_ENVMAP | TRT_FLAG_ROW_QUIRK)
+
+#define TRT_MAX_DEPTH_LIMIT 20u /* MAX_DEPTH of shader.comp:75 */
+
+typedef struct trt_params {
+    uint32_t width, height; /* image size; WIDTH/HEIGHT of main.cpp:35-36 & shader.comp:79-80 */
+    uint32_t max_depth;     /* MAX_DEPTH (shader.comp:75): segments of depth 0..max_depth-1; 1..20 */
+    uint32_t spp;           /* samples per pixel; 1 = the reference's pixel-centre rays */
+    uint32_t seed;          /* jitter seed (spp > 1 only) */
+    uint32_t flags;         /* TRT_FLAG_* */
+    float fov;              /* vertical field of view in radians (main.cpp:1498: 1.05f) */
+    uint32_t band_rows;     /* row-band sharding: 0 = whole image; else rows r with */
+    uint32_t band_count;    /*   (r / band_rows) % band_count == band_index are rendered and */
+    uint32_t band_index;    /*   written compactly, in row order */
+    const trt_ray* rays_in; /* optional binding-1 replay (width*height rays), or NULL */
+} trt_params;
+
+typedef struct trt_stats {
+    uint64_t primary_rays;   /* root segments traced (W*H*spp over the rendered rows) */
+    uint64_t secondary_rays; /* reflection/refraction/TIR segments that reach scene_intersect */
+    uint64_t shadow_rays;    /* shadow_intersect calls */
+    /* Per-stage work, the units of the algorithmic-byte roofline: */
+    uint64_t misses;         /* segments with no hit (background lookups) */
+    uint64_t tri_nearest;    /* segments whose closest hit is a triangle */
+    uint64_t sphere_tests;   /* ray_sphere_intersect calls (scene + shadow) */
+    uint64_t batch_tests;    /* ray_aabb_intersect calls (scene + shadow) */
+    uint64_t batch_hits;     /* ... that passed */
+    uint64_t tri_tests;      /* ray_triangle_intersect calls (scene + shadow) */
+    double kernel_ms;        /* device time of the frame (TRT_FLAG_TIMING) */
+} trt_stats;
+
+typedef struct trt_ctx trt_ctx;
+
+const char* trt_version(void);
+
+/* Creates a context on HIP device `hip_device` (a fresh non-blocking stream). */
+int trt_create(trt_ctx** out, int hip_device);
+int trt_destroy(trt_ctx* ctx);
+const char* trt_last_error(const trt_ctx* ctx);
+
+/* Launch subsequent work on an external hipStream_t (e.g. torch's current stream); NULL
+ * restores the context's own stream. */
+int trt_set_stream(trt_ctx* ctx, void* hip_stream);
+
+/* Uploads the bindings of one scene.  ntri/nmodel may be 0 (the reference cannot bind a
+ * zero-size SSBO; this boundary can), env may be NULL when TRT_FLAG_ENVMAP is never set.
+ * Triangle materials are kept per triangle as in binding 5. */
+int trt_upload_scene(trt_ctx* ctx, const trt_ubo* ubo, const trt_triangle* tris, uint32_t ntri,
+                     const trt_model* models, uint32_t nmodel, const uint8_t* env_rgba8,
+                     uint32_t env_w, uint32_t env_h);
+
+/* Per-frame UBO update (spheres, lights, camera). */
+int trt_update_ubo(trt_ctx* ctx, const trt_ubo* ubo);
+
+/* Renders one frame.  out_rgba8: rows*width*4 bytes (RGBA8 = floor(255*c + 0.5), a = 255);
+ * out_rgba32f: rows*width*4 floats (rayOut.resultColor = (c, 1)).  Either may be NULL.
+ * rows = trt_output_rows(p).  Host pointers unless TRT_FLAG_DEVICE_PTRS; with device
+ * pointers and no COUNT/TIMING flag the call only enqueues work on the stream. */
+int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out_rgba32f,
+               trt_stats* st);
+
+/* Waits for all work enqueued on the context's stream. */
+int trt_synchronize(trt_ctx* ctx);
+
+/* Rows written by trt_render for these params (H, or the band's share). */
+uint32_t trt_output_rows(const trt_params* p);
+
+/* Fills `p` with the reference defaults: 1024x768, depth 20, spp 1, fov 1.05,
+ * TRT_FLAGS_REFERENCE. */
+void trt_params_default(trt_params* p);
+
+/* ---- host scene build (main.cpp:192-252, 1529-1580, 2290-2335) -------------------- */
+
+typedef struct trt_scene trt_scene;
+
+int trt_scene_create(trt_scene** out);
+void trt_scene_destroy(trt_scene* s);
+const char* trt_scene_last_error(const trt_scene* s);
+
+/* Triangles per AABB batch (main.cpp:1549: 64). */
+int trt_scene_set_batch_size(trt_scene* s, uint32_t batch_size);
+
+/* One modelList entry (config.hpp:97-101) from an already-triangulated mesh: positions
+ * (xyz floats, nverts) and indices (3 per triangle, file order).  Applies
+ * M = T * Rz * Ry * Rx * S (transformTriangles, main.cpp:192-216), smooth vertex
+ * normals when normal_interp == 1 (computeVertexNormals, main.cpp:218-252), then splits
+ * into batches with AABBs (main.cpp:1548-1566). */
+int trt_scene_add_mesh(trt_scene* s, const float* positions, uint32_t nverts,
+                       const uint32_t* indices, uint32_t ntris, const trt_material* mat,
+                       const float scale[3], const float rotation_deg[3],
+                       const float translation[3], int normal_interp);
+
+/* The same from an OBJ file (loadObjAsTriangles, main.cpp:2290-2335, with tinyobjloader's
+ * triangulation rules). */
+int trt_scene_add_obj(trt_scene* s, const char* path, const trt_material* mat,
+                      const float scale[3], const float rotation_deg[3],
+                      const float translation[3], int normal_interp);
+
+uint32_t trt_scene_triangle_count(const trt_scene* s);
+uint32_t trt_scene_model_count(const trt_scene* s);
+const trt_triangle* trt_scene_triangles(const trt_scene* s);
+const trt_model* trt_scene_models(const trt_scene* s);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* TRT_ABI_H */

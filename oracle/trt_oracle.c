@@ -1,0 +1,836 @@
+/*
+ * oracle/trt_oracle.c — TEST INFRASTRUCTURE ONLY.  Not part of the product.
+ *
+ * A plain-C (C11, FP32, -ffp-contract=off) restatement of the reference's per-pixel
+ * Whitted tracer, VulkanComputeShaderApplication/shaders/shader.comp (snapshot 2025-07-25),
+ * and of the host primary-ray generation in main.cpp:1496-1506.  Every function cites the
+ * lines it follows.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load it, and only as the checker / CPU baseline; the HIP product never links it.
+ *
+ * PARITY STATUS.  The reference hot path is GLSL compiled by a Vulkan driver; no GLSL
+ * compiler, SPIR-V runtime or Vulkan ICD exists in this image, and the
+ * reference ships no tests or golden images.  This restatement is therefore
+ * "parity unpinned" against the running reference: it is pinned by hand-derived
+ * known-answer vectors (tests/test_oracle_kat.py), by the literal-vs-fast equivalence of
+ * its two modes, and its input stage by goldens from the reference's own vendored
+ * tinyobjloader (oracle/_ref).  GLSL built-ins are realised as: dot = (x*x'+y*y')+z*z',
+ * normalize(v) = v * (1/sqrt(dot(v,v))), length = sqrt(dot), reflect(I,N) = I - (2*dot(N,I))*N,
+ * min/max NaN-ignoring (fminf/fmaxf), pow/atan/acos from libm (acos argument clamped to
+ * [-1,1]), bilinear CLAMP_TO_EDGE texel filtering with float weights.
+ *
+ * Two modes:
+ *   ORC_MODE_LITERAL  the shader as written: the 40-entry PathSegment stack with 32-entry
+ *                     volume stacks copied on every push, Push/Pop (shader.comp:87-195).
+ *   ORC_MODE_FAST     the volume stack deleted (stack_pos is an `in`
+ *                     parameter, so incident = air, outgoing = hit material, leaving = false)
+ *                     and the DFS kept as "current segment + deferred refraction children",
+ *                     which pops segments in exactly the reference order.
+ * tests/ asserts both modes give bit-identical images.
+ */
+#include "trt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+/* ---- constants (shader.comp:75-85) -------------------------------------------------- */
+#define MAX_STACK_SIZE 40 /* MAX_DEPTH * 2, shader.comp:76 */
+#define MIN_EPSILON 0.0001f /* shader.comp:78 */
+#define GAMMA 2.2f /* shader.comp:81 */
+#define PI_F 3.14159265358979323846f /* shader.comp:82 */
+#define MAX_VOLUME_STACK 32 /* shader.comp:93 */
+
+typedef struct { float x, y, z; } v3;
+
+static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mulv(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 muls(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline float dot3(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static inline v3 cross3(v3 a, v3 b) {
+    return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+static inline v3 normalize3(v3 v) { float inv = 1.0f / sqrtf(dot3(v, v)); return muls(v, inv); }
+static inline float length3(v3 v) { return sqrtf(dot3(v, v)); }
+/* GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N */
+static inline v3 reflect3(v3 I, v3 N) { float k = 2.0f * dot3(N, I); return sub(I, muls(N, k)); }
+static inline v3 xyz(trt_vec4 v) { return mk(v.x, v.y, v.z); }
+static inline v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+static inline void st3(float* p, v3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+
+static inline int mat_equal(const trt_material* a, const trt_material* b) {
+    /* isEqualMaterial, shader.comp:96-100 (vec4 ==, so NaN != NaN) */
+    return a->albedo.x == b->albedo.x && a->albedo.y == b->albedo.y &&
+           a->albedo.z == b->albedo.z && a->albedo.w == b->albedo.w &&
+           a->diffuse_specular.x == b->diffuse_specular.x &&
+           a->diffuse_specular.y == b->diffuse_specular.y &&
+           a->diffuse_specular.z == b->diffuse_specular.z &&
+           a->diffuse_specular.w == b->diffuse_specular.w &&
+           a->refractive.x == b->refractive.x && a->refractive.y == b->refractive.y &&
+           a->refractive.z == b->refractive.z && a->refractive.w == b->refractive.w;
+}
+
+static const trt_material AIR = {{0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}}; /* shader.comp:85 */
+
+/* ---- intersection primitives -------------------------------------------------------- */
+
+/* ray_aabb_intersect, shader.comp:197-207 */
+static inline int aabb_hit(v3 o, v3 inv, const trt_vec4* bmin, const trt_vec4* bmax) {
+    float t0x = (bmin->x - o.x) * inv.x, t0y = (bmin->y - o.y) * inv.y, t0z = (bmin->z - o.z) * inv.z;
+    float t1x = (bmax->x - o.x) * inv.x, t1y = (bmax->y - o.y) * inv.y, t1z = (bmax->z - o.z) * inv.z;
+    float tnx = fminf(t0x, t1x), tny = fminf(t0y, t1y), tnz = fminf(t0z, t1z);
+    float tfx = fmaxf(t0x, t1x), tfy = fmaxf(t0y, t1y), tfz = fmaxf(t0z, t1z);
+    float tNear = fmaxf(fmaxf(tnx, tny), tnz);
+    float tFar = fminf(fminf(tfx, tfy), tfz);
+    return tNear <= tFar && tFar > MIN_EPSILON;
+}
+
+/* ray_triangle_intersect, shader.comp:223-270.  want_normal = 0 skips the normal (only
+ * shadow_intersect passes 0, and it never reads it). */
+static inline int tri_hit(v3 o, v3 d, const trt_triangle* tri, int normal_interp,
+                          int want_normal, float* t_out, v3* n_out) {
+    v3 v0 = xyz(tri->v0), v1 = xyz(tri->v1), v2 = xyz(tri->v2);
+    v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    v3 h = cross3(d, e2);
+    float a = dot3(e1, h);
+    if (a > -MIN_EPSILON && a < MIN_EPSILON) return 0;
+    float f = 1.0f / a;
+    v3 s = sub(o, v0);
+    float u = f * dot3(s, h);
+    if (u < 0.0f || u > 1.0f) return 0;
+    v3 q = cross3(s, e1);
+    float v = f * dot3(d, q);
+    if (v < 0.0f || u + v > 1.0f) return 0;
+    float t = f * dot3(e2, q);
+    if (t <= MIN_EPSILON) return 0;
+    *t_out = t;
+    if (want_normal) {
+        if (normal_interp == 0) {
+            *n_out = normalize3(cross3(e1, e2));
+        } else {
+            float w = 1.0f - u - v;
+            v3 n = add(add(muls(xyz(tri->v0_norm), w), muls(xyz(tri->v1_norm), u)),
+                       muls(xyz(tri->v2_norm), v));
+            *n_out = normalize3(n);
+        }
+    }
+    return 1;
+}
+
+/* ray_sphere_intersect, shader.comp:272-285 */
+static inline int sphere_hit(v3 o, v3 d, const trt_sphere* s, float* t) {
+    v3 L = sub(xyz(s->center_radius), o);
+    float tca = dot3(L, d);
+    float d2 = dot3(L, L) - tca * tca;
+    float r2 = s->center_radius.w * s->center_radius.w;
+    if (d2 > r2) return 0;
+    float thc = sqrtf(r2 - d2);
+    float t0 = tca - thc, t1 = tca + thc;
+    if (t0 > MIN_EPSILON) *t = t0;
+    else if (t1 > MIN_EPSILON) *t = t1;
+    else return 0;
+    return 1;
+}
+
+/* custom_refract, shader.comp:209-221 */
+static inline v3 custom_refract(v3 I, v3 N, float eta_out, float eta_in) {
+    int entering = dot3(I, N) < 0.0f;
+    v3 fn = entering ? N : neg(N);
+    float cosi = dot3(neg(I), fn);
+    cosi = fminf(fmaxf(cosi, 0.0f), 1.0f); /* clamp(x, 0, 1) */
+    float eta = entering ? eta_in / eta_out : eta_out / eta_in;
+    float sint2 = eta * eta * (1.0f - cosi * cosi);
+    if (sint2 > 1.0f) return mk(0.0f, 0.0f, 0.0f);
+    float k = sqrtf(1.0f - sint2);
+    v3 r = add(muls(I, eta), muls(fn, eta * cosi - k));
+    return normalize3(r);
+}
+
+/* direction_to_uv, shader.comp:410-416 */
+static inline void dir_to_uv(v3 d, float* u, float* v) {
+    float theta = atan2f(d.z, d.x);
+    float y = fminf(fmaxf(d.y, -1.0f), 1.0f); /* GLSL acos is undefined outside [-1,1] */
+    float phi = acosf(y);
+    *u = (theta + PI_F) / (2.0f * PI_F);
+    *v = phi / PI_F;
+}
+
+/* texture(backgroundImage, uv).rgb, shader.comp:456, with the sampler of main.cpp:1091-1106:
+ * LINEAR, CLAMP_TO_EDGE, level 0, R8G8B8A8_UNORM (main.cpp:955-980). */
+static inline v3 sample_env(const uint8_t* env, uint32_t w, uint32_t h, float u, float v) {
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    if (!(x == x)) x = 0.0f;
+    if (!(y == y)) y = 0.0f;
+    float xf = floorf(x), yf = floorf(y);
+    float a = x - xf, b = y - yf;
+    long ix0 = (long)xf, iy0 = (long)yf;
+    long ix1 = ix0 + 1, iy1 = iy0 + 1;
+    long wm = (long)w - 1, hm = (long)h - 1;
+    ix0 = ix0 < 0 ? 0 : (ix0 > wm ? wm : ix0);
+    ix1 = ix1 < 0 ? 0 : (ix1 > wm ? wm : ix1);
+    iy0 = iy0 < 0 ? 0 : (iy0 > hm ? hm : iy0);
+    iy1 = iy1 < 0 ? 0 : (iy1 > hm ? hm : iy1);
+    const uint8_t* p00 = env + 4 * ((size_t)iy0 * w + (size_t)ix0);
+    const uint8_t* p10 = env + 4 * ((size_t)iy0 * w + (size_t)ix1);
+    const uint8_t* p01 = env + 4 * ((size_t)iy1 * w + (size_t)ix0);
+    const uint8_t* p11 = env + 4 * ((size_t)iy1 * w + (size_t)ix1);
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b);
+    float w01 = (1.0f - a) * b, w11 = a * b;
+    float c[3];
+    for (int k = 0; k < 3; ++k) {
+        float t00 = (float)p00[k] / 255.0f, t10 = (float)p10[k] / 255.0f;
+        float t01 = (float)p01[k] / 255.0f, t11 = (float)p11[k] / 255.0f;
+        c[k] = ((w00 * t00 + w10 * t10) + w01 * t01) + w11 * t11;
+    }
+    return mk(c[0], c[1], c[2]);
+}
+
+/* ---- scene queries ------------------------------------------------------------------ */
+
+typedef struct {
+    int hit;
+    int is_tri; /* closest hit is a triangle (for the tri_nearest counter) */
+    float distance;
+    v3 point, normal;
+    trt_material material;
+} scene_hit;
+
+typedef struct {
+    uint64_t primary, secondary, shadow;
+    uint64_t miss, tri_nearest, sphere_tests, batch_tests, batch_hits, tri_tests;
+} counters;
+
+static inline const trt_sphere* ubo_sphere(const trt_ubo* u, int i) {
+    return i == 0 ? &u->sphere0 : i == 1 ? &u->sphere1 : i == 2 ? &u->sphere2 : &u->sphere3;
+}
+
+/* scene_intersect, shader.comp:295-362 (floor, spheres, batches in index order; strict `<`
+ * so the first candidate wins ties). */
+static void scene_intersect(const orc_scene* sc, uint32_t flags, v3 o, v3 d, scene_hit* nh,
+                            counters* cnt) {
+    nh->hit = 0;
+    nh->is_tri = 0;
+    nh->distance = 1e10f;
+    if (flags & TRT_FLAG_FLOOR) { /* shader.comp:302-320 */
+        if (fabsf(d.y) > MIN_EPSILON) {
+            float t = -(o.y + 4.0f) / d.y;
+            if (t > MIN_EPSILON && t < nh->distance) {
+                v3 p = add(o, muls(d, t));
+                if (fabsf(p.x) < 10.0f && p.z < -5.0f && p.z > -30.0f) {
+                    nh->hit = 1;
+                    nh->is_tri = 0;
+                    nh->distance = t;
+                    nh->point = p;
+                    nh->normal = mk(0.0f, 1.0f, 0.0f);
+                    v3 color = mk(0.3f, 0.3f, 0.3f);
+                    if (flags & TRT_FLAG_CHECKER) { /* shader.comp:312 (commented upstream) */
+                        float m = floorf(p.x * 0.5f + 1024.0f) + floorf(p.z * 0.5f);
+                        float mod2 = m - 2.0f * floorf(m / 2.0f); /* GLSL mod(x, 2.0) */
+                        if (!(mod2 == 0.0f)) color = mk(0.3f, 0.2f, 0.1f);
+                    }
+                    trt_material fm = {{2.0f, 0.0f, 0.0f, 0.0f}, {color.x, color.y, color.z, 1.0f},
+                                       {1.0f, 0.0f, 0.0f, 0.0f}};
+                    nh->material = fm;
+                }
+            }
+        }
+    }
+    if (flags & TRT_FLAG_SPHERES) { /* shader.comp:322-335 */
+        for (int i = 0; i < 4; ++i) {
+            const trt_sphere* s = ubo_sphere(sc->ubo, i);
+            float t = 1e10f;
+            cnt->sphere_tests++;
+            if (sphere_hit(o, d, s, &t) && t < nh->distance) {
+                v3 p = add(o, muls(d, t));
+                nh->hit = 1;
+                nh->is_tri = 0;
+                nh->distance = t;
+                nh->point = p;
+                nh->normal = normalize3(sub(p, xyz(s->center_radius)));
+                nh->material = s->material;
+            }
+        }
+    }
+    v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); /* shader.comp:336 */
+    for (uint32_t i = 0; i < sc->nmodel; ++i) {      /* shader.comp:338-361 */
+        const trt_model* m = &sc->models[i];
+        cnt->batch_tests++;
+        if (!aabb_hit(o, inv, &m->bboxMin, &m->bboxMax)) continue;
+        cnt->batch_hits++;
+        int start = m->params0.x, end = m->params0.x + m->params0.y, ni = m->params0.z;
+        for (int j = start; j < end; ++j) {
+            const trt_triangle* tri = &sc->tris[j];
+            float t;
+            v3 n;
+            cnt->tri_tests++;
+            if (tri_hit(o, d, tri, ni, 1, &t, &n)) {
+                if (t > MIN_EPSILON && t < nh->distance) {
+                    nh->hit = 1;
+                    nh->distance = t;
+                    nh->point = add(o, muls(d, t));
+                    nh->normal = n;
+                    nh->material = tri->material;
+                    nh->is_tri = 1;
+                }
+            }
+        }
+    }
+}
+
+/* shadow_intersect, shader.comp:364-399 (floor excluded; any hit). */
+static int shadow_intersect(const orc_scene* sc, uint32_t flags, v3 o, v3 d, float max_dist,
+                            counters* cnt) {
+    if (flags & TRT_FLAG_SPHERES) {
+        for (int i = 0; i < 4; ++i) {
+            float t = 1e10f;
+            cnt->sphere_tests++;
+            if (sphere_hit(o, d, ubo_sphere(sc->ubo, i), &t) && t < max_dist) return 1;
+        }
+    }
+    v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    for (uint32_t i = 0; i < sc->nmodel; ++i) {
+        const trt_model* m = &sc->models[i];
+        cnt->batch_tests++;
+        if (!aabb_hit(o, inv, &m->bboxMin, &m->bboxMax)) continue;
+        cnt->batch_hits++;
+        int start = m->params0.x, end = m->params0.x + m->params0.y;
+        for (int j = start; j < end; ++j) {
+            float t;
+            v3 n;
+            cnt->tri_tests++;
+            if (tri_hit(o, d, &sc->tris[j], 0, 0, &t, &n) && t > MIN_EPSILON && t < max_dist)
+                return 1;
+        }
+    }
+    return 0;
+}
+
+static inline v3 background(const orc_scene* sc, uint32_t flags, v3 d) {
+    if (flags & TRT_FLAG_ENVMAP) { /* shader.comp:455-456 */
+        float u, v;
+        dir_to_uv(d, &u, &v);
+        return sample_env(sc->env, sc->env_w, sc->env_h, u, v);
+    }
+    return mk(0.2f, 0.7f, 0.8f); /* BACKGROUND_COLOR, shader.comp:77, 457 */
+}
+
+/* Phong + 3 shadow rays, shader.comp:483-507.  Returns diffuse*albedo.x + specular*albedo.y. */
+static v3 shade(const orc_scene* sc, uint32_t flags, const scene_hit* hit, v3 dir, counters* cnt) {
+    const trt_ubo* u = sc->ubo;
+    v3 lights[3] = {xyz(u->light0), xyz(u->light1), xyz(u->light2)};
+    v3 p = hit->point, n = hit->normal, v = neg(dir);
+    v3 diffuse = mk(0, 0, 0), specular = mk(0, 0, 0);
+    v3 kd = xyz(hit->material.diffuse_specular);
+    float ep = MIN_EPSILON;
+    for (int i = 0; i < 3; ++i) {
+        v3 light_dir = normalize3(sub(lights[i], p));
+        float light_dist = length3(sub(lights[i], p));
+        v3 shadow_origin = dot3(light_dir, n) < 0.0f ? sub(p, muls(n, ep)) : add(p, muls(n, ep));
+        cnt->shadow++;
+        if (shadow_intersect(sc, flags, shadow_origin, light_dir, light_dist, cnt)) continue;
+        float diff = 1.0f * fmaxf(0.0f, dot3(n, light_dir));
+        diffuse = add(diffuse, muls(kd, diff));
+        v3 reflect_dir = reflect3(neg(light_dir), n);
+        float spec = 1.0f * powf(fmaxf(0.0f, dot3(reflect_dir, v)), hit->material.diffuse_specular.w);
+        specular = add(specular, muls(kd, spec));
+    }
+    return add(muls(diffuse, hit->material.albedo.x), muls(specular, hit->material.albedo.y));
+}
+
+/* ---- cast_ray, literal (shader.comp:87-195, 401-408, 423-583) ----------------------- */
+
+typedef struct {
+    trt_material material;
+    int topmost, odd_parity;
+} vs_elem; /* VolumeStackElement, shader.comp:87-91 */
+
+typedef struct {
+    v3 origin, direction, throughput;
+    int depth, stack_pos;
+    vs_elem volume_stack[MAX_VOLUME_STACK];
+} path_segment; /* shader.comp:401-408 */
+
+static int find_in_stack(const vs_elem* st, int pos, const trt_material* m) { /* :103-110 */
+    for (int i = pos; i >= 0; i--)
+        if (mat_equal(&st[i].material, m)) return i;
+    return -1;
+}
+
+/* Push, shader.comp:113-152.  stack_pos is an `in` parameter: the increment is local. */
+static void vs_push(vs_elem* st, int stack_pos, const trt_material* m, trt_material* incident,
+                    trt_material* outgoing, int* leaving) {
+    int prev_same = find_in_stack(st, stack_pos, m);
+    int odd_parity = 1;
+    if (prev_same >= 0) {
+        st[prev_same].topmost = 0;
+        odd_parity = !st[prev_same].odd_parity;
+    }
+    int idx = -1;
+    for (int i = stack_pos; i >= 0; i--) {
+        if (!mat_equal(&st[i].material, m) && st[i].odd_parity && st[i].topmost) {
+            idx = i;
+            break;
+        }
+    }
+    if (stack_pos < MAX_VOLUME_STACK - 1) {
+        stack_pos++;
+        st[stack_pos].material = *m;
+        st[stack_pos].topmost = 1;
+        st[stack_pos].odd_parity = odd_parity;
+    }
+    if (odd_parity) {
+        *incident = (idx >= 0) ? st[idx].material : AIR;
+        *outgoing = *m;
+    } else {
+        *outgoing = (idx >= 0) ? st[idx].material : AIR;
+        *incident = (idx < prev_same) ? *m : *outgoing;
+    }
+    *leaving = !odd_parity;
+}
+
+/* Pop, shader.comp:154-195 (stack_pos by value). */
+static void vs_pop(vs_elem* st, int stack_pos, int leaving) {
+    if (stack_pos >= 0) {
+        vs_elem top = st[stack_pos];
+        stack_pos--;
+        if (leaving && stack_pos >= 0) {
+            int idx = -1;
+            for (int i = stack_pos; i >= 0; i--) {
+                if (mat_equal(&st[i].material, &top.material)) { idx = i; break; }
+            }
+            if (idx >= 0) {
+                for (int i = idx + 1; i <= stack_pos; i++) st[i - 1] = st[i];
+                if (stack_pos > 0) stack_pos--;
+            }
+        }
+        for (int i = stack_pos; i >= 0; i--) {
+            if (mat_equal(&st[i].material, &top.material)) { st[i].topmost = 1; break; }
+        }
+    }
+}
+
+static v3 cast_ray_literal(const orc_scene* sc, const trt_params* p, v3 orig, v3 dir,
+                           counters* cnt, path_segment* stack /* [MAX_STACK_SIZE] */) {
+    const int MAX_DEPTH = (int)p->max_depth;
+    v3 color = mk(0, 0, 0);
+    int stackSize = 0;
+    path_segment* root = &stack[stackSize++];
+    root->origin = orig;
+    root->direction = dir;
+    root->throughput = mk(1, 1, 1);
+    root->depth = 0;
+    root->stack_pos = 0;
+    for (int i = 0; i < MAX_VOLUME_STACK; i++) {
+        root->volume_stack[i].material = AIR;
+        root->volume_stack[i].topmost = 0;
+        root->volume_stack[i].odd_parity = 0;
+    }
+    path_segment seg;
+    vs_elem localStack[MAX_VOLUME_STACK];
+    while (stackSize > 0) {
+        seg = stack[--stackSize];
+        if (seg.depth >= MAX_DEPTH || dot3(seg.throughput, seg.throughput) < 0.001f) continue;
+        if (seg.depth == 0) cnt->primary++; else cnt->secondary++;
+        scene_hit hit;
+        scene_intersect(sc, p->flags, seg.origin, seg.direction, &hit, cnt);
+        if (!hit.hit) {
+            cnt->miss++;
+            color = add(color, mulv(seg.throughput, background(sc, p->flags, seg.direction)));
+            continue;
+        }
+        if (hit.is_tri) cnt->tri_nearest++;
+        int localStackSize = seg.stack_pos;
+        memcpy(localStack, seg.volume_stack, sizeof(localStack));
+        trt_material incident, outgoing;
+        int leaving;
+        vs_push(localStack, localStackSize, &hit.material, &incident, &outgoing, &leaving);
+        float eta_out = outgoing.refractive.x, eta_in = incident.refractive.x;
+        /* current_material (shader.comp:475-481) is never read: omitted. */
+        v3 n = hit.normal, pt = hit.point;
+        color = add(color, mulv(seg.throughput, shade(sc, p->flags, &hit, seg.direction, cnt)));
+        float ep = MIN_EPSILON;
+        int skip_reflect = 0;
+        if (hit.material.albedo.w > 0.0f && stackSize < MAX_STACK_SIZE) { /* :513-556 */
+            v3 rd = custom_refract(seg.direction, n, eta_out, eta_in);
+            path_segment* ns = &stack[stackSize];
+            if (length3(rd) > 0.0001f) {
+                rd = normalize3(rd);
+                v3 off = dot3(rd, n) < 0.0f ? muls(neg(n), ep) : muls(n, ep);
+                ns->origin = add(pt, off);
+                ns->direction = rd;
+                ns->throughput = muls(seg.throughput, outgoing.albedo.w);
+                ns->depth = seg.depth + 1;
+                memcpy(ns->volume_stack, localStack, sizeof(localStack));
+                ns->stack_pos = localStackSize;
+                stackSize++;
+            } else {
+                v3 rf = normalize3(reflect3(seg.direction, n));
+                v3 off = dot3(rf, n) < 0.0f ? muls(neg(n), ep) : muls(n, ep);
+                ns->origin = add(pt, off);
+                ns->direction = rf;
+                ns->throughput = muls(seg.throughput, outgoing.albedo.w);
+                ns->depth = seg.depth + 1;
+                memcpy(ns->volume_stack, localStack, sizeof(localStack));
+                ns->stack_pos = localStackSize;
+                vs_pop(ns->volume_stack, ns->stack_pos, leaving);
+                stackSize++;
+                skip_reflect = 1;
+            }
+        }
+        if (hit.material.albedo.z > 0.0f && stackSize < MAX_STACK_SIZE && !skip_reflect) {
+            v3 nd = normalize3(reflect3(seg.direction, n)); /* :558-575 */
+            v3 off = dot3(nd, n) < 0.0f ? muls(neg(n), ep) : muls(n, ep);
+            path_segment* ns = &stack[stackSize];
+            ns->origin = add(pt, off);
+            ns->direction = nd;
+            ns->throughput = muls(seg.throughput, outgoing.albedo.z);
+            ns->depth = seg.depth + 1;
+            memcpy(ns->volume_stack, localStack, sizeof(localStack));
+            ns->stack_pos = localStackSize;
+            vs_pop(ns->volume_stack, ns->stack_pos, leaving);
+            stackSize++;
+        }
+        if (hit.material.albedo.w > 0.0f && leaving && stackSize < MAX_STACK_SIZE)
+            vs_pop(localStack, localStackSize, leaving); /* :577-579 */
+    }
+    /* clamp(color, 0, 1), shader.comp:582 */
+    return mk(fminf(fmaxf(color.x, 0.0f), 1.0f), fminf(fmaxf(color.y, 0.0f), 1.0f),
+              fminf(fmaxf(color.z, 0.0f), 1.0f));
+}
+
+/* ---- cast_ray, fast ------------------------------------------------------------------ */
+
+typedef struct {
+    v3 origin, direction;
+    float thr; /* throughput is always (s,s,s): vec3(1) times scalar albedo weights */
+    int depth;
+} seg_fast;
+
+static int seg_alive(float thr, int depth, int max_depth) {
+    float tt = (thr * thr + thr * thr) + thr * thr; /* dot(thr, thr), shader.comp:449 */
+    return depth < max_depth && !(tt < 0.001f);
+}
+
+static v3 cast_ray_fast(const orc_scene* sc, const trt_params* p, v3 orig, v3 dir, counters* cnt) {
+    const int D = (int)p->max_depth;
+    v3 color = mk(0, 0, 0);
+    seg_fast deferred[TRT_MAX_DEPTH_LIMIT + 2];
+    int nd = 0;
+    seg_fast cur = {orig, dir, 1.0f, 0};
+    for (;;) {
+        int have_next = 0;
+        seg_fast next;
+        if (seg_alive(cur.thr, cur.depth, D)) {
+            if (cur.depth == 0) cnt->primary++; else cnt->secondary++;
+            scene_hit hit;
+            scene_intersect(sc, p->flags, cur.origin, cur.direction, &hit, cnt);
+            if (!hit.hit) {
+                cnt->miss++;
+                color = add(color, muls(background(sc, p->flags, cur.direction), cur.thr));
+            } else {
+                if (hit.is_tri) cnt->tri_nearest++;
+                v3 n = hit.normal, pt = hit.point;
+                v3 c = shade(sc, p->flags, &hit, cur.direction, cnt);
+                color = add(color, muls(c, cur.thr));
+                const trt_material* m = &hit.material;
+                float ep = MIN_EPSILON;
+                int nkids = 0;
+                seg_fast kid_refr = {{0, 0, 0}, {0, 0, 0}, 0.0f, 0}, kid_refl = kid_refr;
+                int skip_reflect = 0;
+                if (m->albedo.w > 0.0f) {
+                    v3 rd = custom_refract(cur.direction, n, m->refractive.x, 1.0f);
+                    if (length3(rd) > 0.0001f) {
+                        rd = normalize3(rd);
+                    } else {
+                        rd = normalize3(reflect3(cur.direction, n));
+                        skip_reflect = 1;
+                    }
+                    v3 off = dot3(rd, n) < 0.0f ? muls(neg(n), ep) : muls(n, ep);
+                    kid_refr.origin = add(pt, off);
+                    kid_refr.direction = rd;
+                    kid_refr.thr = cur.thr * m->albedo.w;
+                    kid_refr.depth = cur.depth + 1;
+                    nkids |= 1;
+                }
+                if (m->albedo.z > 0.0f && !skip_reflect) {
+                    v3 rd = normalize3(reflect3(cur.direction, n));
+                    v3 off = dot3(rd, n) < 0.0f ? muls(neg(n), ep) : muls(n, ep);
+                    kid_refl.origin = add(pt, off);
+                    kid_refl.direction = rd;
+                    kid_refl.thr = cur.thr * m->albedo.z;
+                    kid_refl.depth = cur.depth + 1;
+                    nkids |= 2;
+                }
+                /* The reference pushes refraction then reflection and pops the reflection
+                 * first; the refraction child waits on the deferred stack. */
+                if (nkids == 3) {
+                    deferred[nd++] = kid_refr;
+                    next = kid_refl;
+                    have_next = 1;
+                } else if (nkids == 1) {
+                    next = kid_refr;
+                    have_next = 1;
+                } else if (nkids == 2) {
+                    next = kid_refl;
+                    have_next = 1;
+                }
+            }
+        }
+        if (have_next) {
+            cur = next;
+        } else if (nd > 0) {
+            cur = deferred[--nd];
+        } else {
+            break;
+        }
+    }
+    return mk(fminf(fmaxf(color.x, 0.0f), 1.0f), fminf(fmaxf(color.y, 0.0f), 1.0f),
+              fminf(fmaxf(color.z, 0.0f), 1.0f));
+}
+
+/* ---- primary rays (main.cpp:1496-1506, shader.comp:592-595) -------------------------- */
+
+static uint32_t pcg_hash(uint32_t v) {
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+
+static double ray_dz(const trt_params* p) {
+    /* dir_z = -1.0 * (HEIGHT / (2.0 * tan(fov / 2.0))), double, main.cpp:1503 */
+    return -1.0 * ((double)p->height / (2.0 * tan((double)p->fov / 2.0)));
+}
+
+static v3 primary_dir(const trt_params* p, float dz, uint32_t x, uint32_t y, uint32_t sample) {
+    uint32_t W = p->width, H = p->height;
+    uint64_t pix = (uint64_t)y * W + x;
+    v3 d;
+    if (p->rays_in) {
+        d = xyz(p->rays_in[pix].dir); /* binding 1, shader.comp:592 */
+    } else {
+        /* main.cpp:1501-1502: `pix++ % WIDTH` then `pix / WIDTH` => row of pixel pix+1 */
+        uint64_t row = (p->flags & TRT_FLAG_ROW_QUIRK) ? (pix + 1) / W : y;
+        float dx, dy;
+        if (p->spp <= 1) {
+            dx = (float)(((double)x + 0.5) - (double)W / 2.0);
+            dy = (float)(-((double)row + 0.5) + (double)H / 2.0);
+        } else { /* build extension: PCG-jittered sub-pixel positions */
+            uint32_t k = pcg_hash(p->seed ^ 0x9E3779B9u);
+            uint32_t a = pcg_hash(k + (uint32_t)pix);
+            uint32_t b = pcg_hash(a + sample);
+            uint32_t c = pcg_hash(b);
+            float jx = (float)(b >> 8) * (1.0f / 16777216.0f);
+            float jy = (float)(c >> 8) * (1.0f / 16777216.0f);
+            dx = ((float)x + jx) - (float)W * 0.5f;
+            dy = (float)H * 0.5f - ((float)row + jy);
+        }
+        d = normalize3(mk(dx, dy, dz)); /* glm::normalize on the host, main.cpp:1504 */
+    }
+    return normalize3(d); /* normalize(ray.dir.xyz), shader.comp:593 */
+}
+
+/* ---- frame driver ------------------------------------------------------------------- */
+
+static int row_selected(const trt_params* p, uint32_t r) {
+    if (p->band_rows == 0 || p->band_count <= 1) return 1;
+    return (r / p->band_rows) % p->band_count == p->band_index;
+}
+
+typedef struct {
+    const orc_scene* sc;
+    const trt_params* p;
+    int mode;
+    const uint32_t* rows; /* selected image rows, in output order */
+    uint32_t nrows;
+    float dz;
+    _Atomic uint32_t next_row;
+    uint8_t* out8;
+    float* out32;
+    _Atomic uint64_t acc[9];
+} job_t;
+
+static void render_row(job_t* J, uint32_t k, counters* cnt, path_segment* lit_stack) {
+    const trt_params* p = J->p;
+    uint32_t y = J->rows[k], W = p->width;
+    v3 orig = xyz(J->sc->ubo->camPos); /* shader.comp:595 */
+    uint32_t spp = p->spp ? p->spp : 1;
+    for (uint32_t x = 0; x < W; ++x) {
+        v3 acc = mk(0, 0, 0);
+        for (uint32_t s = 0; s < spp; ++s) {
+            v3 d = primary_dir(p, J->dz, x, y, s);
+            v3 c = J->mode == ORC_MODE_LITERAL ? cast_ray_literal(J->sc, p, orig, d, cnt, lit_stack)
+                                               : cast_ray_fast(J->sc, p, orig, d, cnt);
+            acc = spp == 1 ? c : add(acc, c);
+        }
+        if (spp > 1) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
+        /* pow(color, vec3(GAMMA)), shader.comp:598 */
+        v3 g = mk(powf(acc.x, GAMMA), powf(acc.y, GAMMA), powf(acc.z, GAMMA));
+        size_t o = (size_t)k * W + x;
+        if (J->out32) { /* rayOut[idx].resultColor = vec4(color, 1.0), shader.comp:601 */
+            J->out32[4 * o + 0] = g.x;
+            J->out32[4 * o + 1] = g.y;
+            J->out32[4 * o + 2] = g.z;
+            J->out32[4 * o + 3] = 1.0f;
+        }
+        if (J->out8) { /* UNORM8 store of the rgba8 image, shader.comp:61, 600 */
+            J->out8[4 * o + 0] = (uint8_t)floorf(g.x * 255.0f + 0.5f);
+            J->out8[4 * o + 1] = (uint8_t)floorf(g.y * 255.0f + 0.5f);
+            J->out8[4 * o + 2] = (uint8_t)floorf(g.z * 255.0f + 0.5f);
+            J->out8[4 * o + 3] = 255;
+        }
+    }
+}
+
+static void* worker(void* arg) {
+    job_t* J = (job_t*)arg;
+    counters cnt;
+    memset(&cnt, 0, sizeof(cnt));
+    path_segment* lit = NULL;
+    if (J->mode == ORC_MODE_LITERAL) lit = (path_segment*)malloc(sizeof(path_segment) * MAX_STACK_SIZE);
+    for (;;) {
+        uint32_t k = atomic_fetch_add(&J->next_row, 1u);
+        if (k >= J->nrows) break;
+        render_row(J, k, &cnt, lit);
+    }
+    free(lit);
+    const uint64_t v[9] = {cnt.primary, cnt.secondary, cnt.shadow, cnt.miss, cnt.tri_nearest,
+                           cnt.sphere_tests, cnt.batch_tests, cnt.batch_hits, cnt.tri_tests};
+    for (int i = 0; i < 9; ++i) atomic_fetch_add(&J->acc[i], v[i]);
+    return NULL;
+}
+
+int orc_render(const orc_scene* sc, const trt_params* p, int mode, int nthreads, uint8_t* out8,
+               float* out32, trt_stats* st) {
+    if (!sc || !p || !sc->ubo) return TRT_ERR_INVALID;
+    if (p->width == 0 || p->height == 0) return TRT_ERR_INVALID;
+    if (p->max_depth < 1 || p->max_depth > TRT_MAX_DEPTH_LIMIT) return TRT_ERR_INVALID;
+    if (p->flags & TRT_FLAG_DEVICE_PTRS) return TRT_ERR_INVALID;
+    if (p->band_rows && p->band_count > 1 && p->band_index >= p->band_count) return TRT_ERR_INVALID;
+    if ((p->flags & TRT_FLAG_ENVMAP) && (!sc->env || sc->env_w == 0 || sc->env_h == 0))
+        return TRT_ERR_INVALID;
+    if ((sc->ntri && !sc->tris) || (sc->nmodel && !sc->models)) return TRT_ERR_INVALID;
+    for (uint32_t i = 0; i < sc->nmodel; ++i) {
+        int64_t s = sc->models[i].params0.x, c = sc->models[i].params0.y;
+        if (s < 0 || c < 0 || s + c > (int64_t)sc->ntri) return TRT_ERR_INVALID;
+    }
+    uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * p->height);
+    if (!rows) return TRT_ERR_OOM;
+    uint32_t nrows = 0;
+    for (uint32_t r = 0; r < p->height; ++r)
+        if (row_selected(p, r)) rows[nrows++] = r;
+    job_t J;
+    J.sc = sc;
+    J.p = p;
+    J.mode = mode;
+    J.rows = rows;
+    J.nrows = nrows;
+    J.dz = (float)ray_dz(p);
+    atomic_init(&J.next_row, 0u);
+    J.out8 = out8;
+    J.out32 = out32;
+    for (int i = 0; i < 9; ++i) atomic_init(&J.acc[i], 0);
+    if (nthreads <= 0) {
+        long n = sysconf(_SC_NPROCESSORS_ONLN);
+        nthreads = n > 0 ? (int)n : 1;
+    }
+    if (nthreads > 256) nthreads = 256;
+    if ((uint32_t)nthreads > nrows) nthreads = nrows ? (int)nrows : 1;
+    pthread_t th[256];
+    int started = 0;
+    for (int i = 1; i < nthreads; ++i)
+        if (pthread_create(&th[started], NULL, worker, &J) == 0) started++;
+    worker(&J);
+    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+    free(rows);
+    if (st) {
+        uint64_t* dst[9] = {&st->primary_rays, &st->secondary_rays, &st->shadow_rays, &st->misses,
+                            &st->tri_nearest, &st->sphere_tests, &st->batch_tests, &st->batch_hits,
+                            &st->tri_tests};
+        for (int i = 0; i < 9; ++i) *dst[i] = atomic_load(&J.acc[i]);
+        st->kernel_ms = 0.0;
+    }
+    return TRT_OK;
+}
+
+/* ---- single-ray probes for the known-answer tests ------------------------------------ */
+
+int orc_ray_aabb(const float o[3], const float d[3], const float bmin[3], const float bmax[3]) {
+    v3 dd = ld3(d);
+    v3 inv = mk(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+    trt_vec4 a = {bmin[0], bmin[1], bmin[2], 1.0f}, b = {bmax[0], bmax[1], bmax[2], 1.0f};
+    return aabb_hit(ld3(o), inv, &a, &b);
+}
+
+int orc_ray_triangle(const float o[3], const float d[3], const float v0[3], const float v1[3],
+                     const float v2[3], const float n0[3], const float n1[3], const float n2[3],
+                     int normal_interp, float* t, float normal[3]) {
+    trt_triangle tri;
+    memset(&tri, 0, sizeof(tri));
+    tri.v0 = (trt_vec4){v0[0], v0[1], v0[2], 1.0f};
+    tri.v1 = (trt_vec4){v1[0], v1[1], v1[2], 1.0f};
+    tri.v2 = (trt_vec4){v2[0], v2[1], v2[2], 1.0f};
+    if (n0) tri.v0_norm = (trt_vec4){n0[0], n0[1], n0[2], 0.0f};
+    if (n1) tri.v1_norm = (trt_vec4){n1[0], n1[1], n1[2], 0.0f};
+    if (n2) tri.v2_norm = (trt_vec4){n2[0], n2[1], n2[2], 0.0f};
+    v3 n = mk(0, 0, 0);
+    float tt = 0.0f;
+    int h = tri_hit(ld3(o), ld3(d), &tri, normal_interp, 1, &tt, &n);
+    if (h) {
+        *t = tt;
+        st3(normal, n);
+    }
+    return h;
+}
+
+int orc_ray_sphere(const float o[3], const float d[3], const float cr[4], float* t) {
+    trt_sphere s;
+    memset(&s, 0, sizeof(s));
+    s.center_radius = (trt_vec4){cr[0], cr[1], cr[2], cr[3]};
+    return sphere_hit(ld3(o), ld3(d), &s, t);
+}
+
+void orc_custom_refract(const float I[3], const float N[3], float eta_out, float eta_in, float out[3]) {
+    st3(out, custom_refract(ld3(I), ld3(N), eta_out, eta_in));
+}
+
+void orc_direction_to_uv(const float d[3], float uv[2]) { dir_to_uv(ld3(d), &uv[0], &uv[1]); }
+
+void orc_sample_env(const uint8_t* env, uint32_t w, uint32_t h, const float uv[2], float rgb[3]) {
+    st3(rgb, sample_env(env, w, h, uv[0], uv[1]));
+}
+
+void orc_primary_dir(const trt_params* p, uint32_t x, uint32_t y, uint32_t sample, float d[3]) {
+    st3(d, primary_dir(p, (float)ray_dz(p), x, y, sample));
+}
+
+void orc_cast_ray(const orc_scene* sc, const trt_params* p, int mode, const float o[3],
+                  const float d[3], float rgb[3], trt_stats* st) {
+    counters cnt;
+    memset(&cnt, 0, sizeof(cnt));
+    v3 c;
+    if (mode == ORC_MODE_LITERAL) {
+        path_segment* lit = (path_segment*)malloc(sizeof(path_segment) * MAX_STACK_SIZE);
+        c = cast_ray_literal(sc, p, ld3(o), ld3(d), &cnt, lit);
+        free(lit);
+    } else {
+        c = cast_ray_fast(sc, p, ld3(o), ld3(d), &cnt);
+    }
+    st3(rgb, c);
+    if (st) {
+        st->primary_rays = cnt.primary;
+        st->secondary_rays = cnt.secondary;
+        st->shadow_rays = cnt.shadow;
+        st->misses = cnt.miss;
+        st->tri_nearest = cnt.tri_nearest;
+        st->sphere_tests = cnt.sphere_tests;
+        st->batch_tests = cnt.batch_tests;
+        st->batch_hits = cnt.batch_hits;
+        st->tri_tests = cnt.tri_tests;
+        st->kernel_ms = 0.0;
+    }
+}

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP kernel (through the C-ABI) against the CPU oracle on the same seeded
+inputs.  Bar: RGBA8 within 1 LSB per channel, rayOut floats within FLOAT_TOL, and the ray
+counts (which depend only on geometry) EXACTLY equal.  Run with `pytest -m gpu`."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.helpers import assert_float_close, assert_rgba8_close
+from vkcomputeshader_tinyraytracer_amd import TrtError, scene as S, types as T
+
+pytestmark = pytest.mark.gpu
+
+SMALL_ENV = (1024, 512)
+
+
+def _counts(st):
+    return (st["primary_rays"], st["secondary_rays"], st["shadow_rays"])
+
+
+def _check(r, sc, params=None, want32=True, max_frac=0.02):
+    p = params if params is not None else sc.params()
+    r.upload_scene(sc)
+    g8, g32, gst = r.draw_frame(p, want32=want32, count=True)
+    o8, o32, ost = orc.render(sc, p, want32=want32)
+    assert _counts(gst) == _counts(ost), (gst, ost)
+    rep = assert_rgba8_close(g8, o8, max_frac=max_frac)
+    if want32:
+        assert_float_close(g32, o32)
+    return rep, gst
+
+
+def test_c1_full_frame(gpu_renderer):
+    rep, st = _check(gpu_renderer, S.config_c1())
+    assert st["primary_rays"] == 1024 * 768 and st["secondary_rays"] == 0
+
+
+def test_c2_full_frame_reference_envmap_size(gpu_renderer):
+    """Headline config at full size: 1024x768, depth 4, 7616x3808 envmap."""
+    rep, st = _check(gpu_renderer, S.config_c2())
+    assert st["secondary_rays"] > 0
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 8, 12, 20])
+def test_c2_depths(gpu_renderer, depth):
+    """Every deferred-stack instantiation (register shift-stack and private array)."""
+    sc = S.config_c2(256, 192, env_size=SMALL_ENV)
+    sc.max_depth = depth
+    _check(gpu_renderer, sc)
+
+
+def test_c3_mesh(gpu_renderer):
+    _check(gpu_renderer, S.config_c3(480, 270, env_size=SMALL_ENV))
+
+
+def test_c4_many_batches(gpu_renderer):
+    _check(gpu_renderer, S.config_c4(384, 216, env_size=SMALL_ENV))
+
+
+def test_reference_default_scene(gpu_renderer, golden_meshes):
+    """The shipped frame: glass+water+ice, spheres off, floor on, MAX_DEPTH 20."""
+    sc = S.config_reference_default(golden_meshes, env_size=SMALL_ENV, width=256, height=192)
+    assert len(sc.tris) == 37956 and len(sc.models) == 594
+    _check(gpu_renderer, sc)
+
+
+def test_readme_scene_rotated_models(gpu_renderer, golden_meshes):
+    """README-era scene (config.hpp:96): rotated + flat-shaded models, checker floor."""
+    tris, models = S.build_models(S.README_MODEL_LIST, golden_meshes)
+    sc = S.Scene("readme", S.make_ubo(), tris, models, S.cached_envmap(*SMALL_ENV), 200, 150, 6,
+                 flags=T.FLAG_FLOOR | T.FLAG_CHECKER | T.FLAG_ENVMAP | T.FLAG_ROW_QUIRK)
+    _check(gpu_renderer, sc)
+
+
+@pytest.mark.parametrize("spp", [2, 4])
+def test_jittered_spp(gpu_renderer, spp):
+    sc = S.config_c2(160, 120, env_size=SMALL_ENV)
+    sc.spp = spp
+    _check(gpu_renderer, sc)
+
+
+@pytest.mark.parametrize("flags", [
+    0,
+    T.FLAG_FLOOR,
+    T.FLAG_SPHERES,
+    T.FLAG_SPHERES | T.FLAG_FLOOR | T.FLAG_CHECKER,
+    T.FLAG_SPHERES | T.FLAG_ENVMAP,
+])
+def test_flag_combinations(gpu_renderer, flags):
+    sc = S.config_c2(128, 96, env_size=SMALL_ENV)
+    sc.flags = flags
+    _check(gpu_renderer, sc)
+
+
+def test_row_quirk_off(gpu_renderer):
+    sc = S.config_c2(128, 96, env_size=SMALL_ENV)
+    sc.flags &= ~T.FLAG_ROW_QUIRK
+    _check(gpu_renderer, sc)
+
+
+def test_ragged_sizes(gpu_renderer):
+    """Image sizes that are not multiples of the 16x16 workgroup tile."""
+    for w, h in [(1, 1), (17, 5), (33, 65), (100, 3)]:
+        sc = S.config_c2(w, h, env_size=SMALL_ENV)
+        _check(gpu_renderer, sc)
+
+
+def test_bands_equal_rows_of_full_frame(gpu_renderer):
+    sc = S.config_c2(128, 100, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    full, _, _ = gpu_renderer.draw_frame(sc.params())
+    for count in (2, 3, 8):
+        parts = []
+        for idx in range(count):
+            p = sc.params(band_rows=8, band_count=count, band_index=idx)
+            band, _, _ = gpu_renderer.draw_frame(p)
+            rows = T.output_rows(sc.height, 8, count, idx)
+            assert band.shape[0] == len(rows)
+            assert np.array_equal(band, full[rows])
+            parts.append(rows)
+        assert sorted(sum(parts, [])) == list(range(sc.height))
+
+
+def test_rays_in_replay(gpu_renderer):
+    """Binding 1 replay: host rays built as main.cpp:1496-1506 does give the same frame."""
+    sc = S.config_c2(96, 64, env_size=SMALL_ENV)
+    p = sc.params()
+    rays = np.zeros(p.width * p.height, T.RAY)
+    for y in range(p.height):
+        for x in range(p.width):
+            rays[y * p.width + x]["dir"] = (*_host_ray(p, x, y), 1.0)
+    gpu_renderer.upload_scene(sc)
+    a, _, _ = gpu_renderer.draw_frame(p)
+    b, _, _ = gpu_renderer.draw_frame(p, rays_in=rays)
+    assert np.array_equal(a, b)
+
+
+def _host_ray(p, x, y):
+    """Host primary ray exactly as main.cpp:1499-1505 (double, then glm::normalize in float)."""
+    W, H = p.width, p.height
+    pix = y * W + x
+    dx = np.float32((pix % W + 0.5) - W / 2.0)
+    dy = np.float32(-((pix + 1) // W + 0.5) + H / 2.0)
+    dz = np.float32(-1.0 * (H / (2.0 * np.tan(np.float64(np.float32(p.fov)) / 2.0))))
+    s = (dx * dx + dy * dy) + dz * dz
+    inv = np.float32(1.0) / np.sqrt(np.float32(s))
+    return dx * inv, dy * inv, dz * inv
+
+
+def test_device_pointers_torch(gpu_renderer):
+    torch = pytest.importorskip("torch")
+    sc = S.config_c2(160, 96, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    host8, host32, _ = gpu_renderer.draw_frame(sc.params(), want32=True)
+    out8 = torch.empty((96, 160, 4), dtype=torch.uint8, device="cuda")
+    out32 = torch.empty((96, 160, 4), dtype=torch.float32, device="cuda")
+    gpu_renderer.set_stream(torch.cuda.current_stream())
+    gpu_renderer.draw_frame(sc.params(), out8=out8, out32=out32)
+    torch.cuda.synchronize()
+    gpu_renderer.set_stream(None)
+    assert np.array_equal(out8.cpu().numpy(), host8)
+    assert np.array_equal(out32.cpu().numpy(), host32)
+
+
+def test_deterministic(gpu_renderer):
+    sc = S.config_c3(200, 120, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    a, _, sa = gpu_renderer.draw_frame(sc.params(), count=True)
+    b, _, sb = gpu_renderer.draw_frame(sc.params(), count=True)
+    assert np.array_equal(a, b) and sa == sb
+
+
+def test_update_ubo_moves_camera(gpu_renderer):
+    """updateUniformBuffer (main.cpp:2165-2179): a new camPos without re-uploading geometry."""
+    sc = S.config_c2(128, 96, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    sc2 = S.config_c2(128, 96, env_size=SMALL_ENV)
+    sc2.ubo = S.make_ubo(cam=(0.5, 0.25, -1.0))
+    gpu_renderer.update_ubo(sc2.ubo)
+    g8, _, _ = gpu_renderer.draw_frame(sc2.params())
+    o8, _, _ = orc.render(sc2, sc2.params())
+    assert_rgba8_close(g8, o8)
+
+
+def test_errors(gpu_renderer):
+    sc = S.config_c2(64, 48, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    with pytest.raises(TrtError):
+        gpu_renderer.draw_frame(sc.params(max_depth=0))
+    with pytest.raises(TrtError):
+        gpu_renderer.draw_frame(sc.params(max_depth=21))
+    with pytest.raises(TrtError):
+        gpu_renderer.draw_frame(sc.params(band_rows=8, band_count=2, band_index=2))
+    bad = S.Scene("bad", S.make_ubo(), sc.tris, np.zeros(1, T.MODEL))
+    bad.models["params0"] = (0, 5, 0, 0)  # range beyond the (empty) triangle buffer
+    with pytest.raises(TrtError):
+        gpu_renderer.upload_scene(bad)
+    no_env = S.Scene("noenv", S.make_ubo(), flags=T.FLAG_ENVMAP)
+    gpu_renderer.upload_scene(no_env)
+    with pytest.raises(TrtError):
+        gpu_renderer.draw_frame(no_env.params(width=8, height=8))

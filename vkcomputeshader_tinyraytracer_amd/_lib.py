@@ -1,0 +1,94 @@
+"""ctypes binding of the product library libtrt.so (include/trt/abi.h).
+
+There is no fallback: if the in-tree HIP library is missing or fails to load, every entry
+point raises.  The CPU oracle under oracle/ is test infrastructure and is never imported
+from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+from .types import Params, Stats
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libtrt.so"
+
+_lib: ctypes.CDLL | None = None
+
+
+class TrtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"trt error {code}: {msg}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Loads libtrt.so (built by __graft_entry__.build() / `make -C .../csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback"
+        )
+    L = ctypes.CDLL(os.fspath(LIB_PATH))
+    c_int, c_u32, vp = ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p
+    f3 = ctypes.POINTER(ctypes.c_float)
+    sigs = {
+        "trt_version": (ctypes.c_char_p, []),
+        "trt_create": (c_int, [ctypes.POINTER(vp), c_int]),
+        "trt_destroy": (c_int, [vp]),
+        "trt_last_error": (ctypes.c_char_p, [vp]),
+        "trt_set_stream": (c_int, [vp, vp]),
+        "trt_upload_scene": (c_int, [vp, vp, vp, c_u32, vp, c_u32, vp, c_u32, c_u32]),
+        "trt_update_ubo": (c_int, [vp, vp]),
+        "trt_render": (c_int, [vp, ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)]),
+        "trt_synchronize": (c_int, [vp]),
+        "trt_output_rows": (c_u32, [ctypes.POINTER(Params)]),
+        "trt_params_default": (None, [ctypes.POINTER(Params)]),
+        "trt_scene_create": (c_int, [ctypes.POINTER(vp)]),
+        "trt_scene_destroy": (None, [vp]),
+        "trt_scene_last_error": (ctypes.c_char_p, [vp]),
+        "trt_scene_set_batch_size": (c_int, [vp, c_u32]),
+        "trt_scene_add_mesh": (c_int, [vp, vp, c_u32, vp, c_u32, vp, f3, f3, f3, c_int]),
+        "trt_scene_add_obj": (c_int, [vp, ctypes.c_char_p, vp, f3, f3, f3, c_int]),
+        "trt_scene_triangle_count": (c_u32, [vp]),
+        "trt_scene_model_count": (c_u32, [vp]),
+        "trt_scene_triangles": (vp, [vp]),
+        "trt_scene_models": (vp, [vp]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+# Every symbol include/trt/abi.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = (
+    "trt_version",
+    "trt_create",
+    "trt_destroy",
+    "trt_last_error",
+    "trt_set_stream",
+    "trt_upload_scene",
+    "trt_update_ubo",
+    "trt_render",
+    "trt_synchronize",
+    "trt_output_rows",
+    "trt_params_default",
+    "trt_scene_create",
+    "trt_scene_destroy",
+    "trt_scene_last_error",
+    "trt_scene_set_batch_size",
+    "trt_scene_add_mesh",
+    "trt_scene_add_obj",
+    "trt_scene_triangle_count",
+    "trt_scene_model_count",
+    "trt_scene_triangles",
+    "trt_scene_models",
+)

@@ -1,0 +1,84 @@
+// trt_device.h — device-side data layout and launch arguments of the CDNA4 tracer.
+//
+// The reference binds AoS std140 records (Triangle 144 B, Model 96 B; shader.comp:19-38)
+// and reads a whole 144-byte Triangle per test (shader.comp:345).  On gfx950 the hot loops
+// are wave-uniform walks over batches and their triangles, so the layouts below are
+// shaped for the SCALAR memory path: one batch record (32 B) and one triangle geometry
+// record (48 B) are each a single s_load_dwordx8 / dwordx4 stream shared by the 64 lanes,
+// and everything a test does not need (materials, vertex normals) lives in separate
+// arrays read once per closest hit.
+#pragma once
+
+#include <stdint.h>
+
+namespace trt {
+
+// One AABB batch (Model, shader.comp:29-38): bbox + triangle range + smooth flag.
+struct alignas(32) BatchRec {
+    float bmin[3];
+    float bmax[3];
+    int32_t start;
+    int32_t count_ni; // count | (normal_interp != 0) << 31
+};
+static_assert(sizeof(BatchRec) == 32, "BatchRec is one s_load_dwordx8");
+
+// Triangle geometry for the Moller-Trumbore test: v0 and the two edges, pre-subtracted
+// on the host with the same float subtraction the shader performs (shader.comp:230-231).
+struct alignas(16) TriGeo {
+    float v0[3];
+    float e1[3];
+    float e2[3];
+    float pad[3];
+};
+static_assert(sizeof(TriGeo) == 48, "TriGeo is 3 x dwordx4");
+
+// Per-triangle shading data, read once per closest hit.
+struct alignas(16) TriShade {
+    float n0[3];
+    float n1[3];
+    float n2[3];
+    uint32_t material; // index into the deduplicated material table
+    uint32_t pad[2];
+};
+static_assert(sizeof(TriShade) == 48, "TriShade is 3 x dwordx4");
+
+struct Mat {
+    float albedo[4];
+    float kd[3];
+    float spec_exp;
+    float ior;
+    float pad[3];
+};
+static_assert(sizeof(Mat) == 48, "Mat is 48 B");
+
+struct SphereArg {
+    float c[3];
+    float r;
+    Mat m;
+};
+
+// Kernel arguments: the UBO (binding 0) travels in the kernarg segment, i.e. in SGPRs.
+struct KArgs {
+    uint32_t width, height;
+    uint32_t rows;      // rows this launch renders (compact output rows)
+    uint32_t band_rows; // 0 = no banding
+    uint32_t band_count, band_index;
+    uint32_t max_depth, spp, seed, flags;
+    float dz;
+    uint32_t nbatch;
+    float cam[3];
+    float light[3][3];
+    SphereArg sph[4];
+    const BatchRec* __restrict__ batches;
+    const TriGeo* __restrict__ geo;
+    const TriShade* __restrict__ shade;
+    const Mat* __restrict__ mats;
+    const uint32_t* __restrict__ env; // RGBA8 texels
+    uint32_t env_w, env_h;
+    const float* __restrict__ rays_in; // Ray records (8 floats), or null
+    uint32_t* __restrict__ out8;       // packed RGBA8, or null
+    float* __restrict__ out32;         // float4 per pixel, or null
+    unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
+};
+
+} // namespace trt

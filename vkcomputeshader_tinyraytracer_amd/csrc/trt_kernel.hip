@@ -1,0 +1,569 @@
+// trt_kernel.hip — the CDNA4 (gfx950) Whitted tracer: the hot path of the reference's
+// compute shader (VulkanComputeShaderApplication/shaders/shader.comp:1-602) rebuilt for
+// MI355X.
+//
+// Execution model
+//   * One lane per pixel (per sample when spp > 1); a wave64 owns an 8x8 pixel tile and a
+//     256-thread workgroup a 16x16 tile, so a wave's rays stay coherent and the batch /
+//     triangle walks below are shared by all 64 lanes.
+//   * The UBO (spheres, lights, camera; binding 0) rides in the kernarg segment (SGPRs).
+//   * scene_intersect / shadow_intersect walk the AABB batches in index order exactly as
+//     shader.comp:338-361 / 379-396 do, but wave-uniformly: a batch record is one scalar
+//     load shared by the wave, `__ballot` over the lanes' slab tests skips a batch no lane
+//     hits, and the hit batch's triangles are streamed as wave-uniform scalar loads
+//     (v0, e1, e2 pre-subtracted on the host with the shader's own subtraction).
+//   * The reference's 40-entry PathSegment stack with 32-entry volume stacks (~80 KB of
+//     private memory per invocation) becomes "current segment + deferred
+//     refraction children": the volume stack is provably inert and the
+//     pop order (reflection before refraction, shader.comp:530/551/573) is preserved, so
+//     colours accumulate in the reference order.  For max_depth <= 5 the deferred stack is
+//     a register shift-stack; deeper trees use a small private array.
+//   * Arithmetic contract shared with the CPU oracle: FP32, no contraction
+//     (-ffp-contract=off), IEEE-correct division and square root, NaN-ignoring min/max.
+#include <hip/hip_runtime.h>
+
+#include "../../include/trt/abi.h"
+#include "trt_device.h"
+
+namespace trt {
+
+#define TRT_EPS 0.0001f /* MIN_EPSILON, shader.comp:78 */
+#define TRT_PI 3.14159265358979323846f /* PI, shader.comp:82 */
+#define TRT_GAMMA 2.2f /* GAMMA, shader.comp:81 */
+
+struct f3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ f3 cross3(f3 a, f3 b) {
+    return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ f3 normalize3(f3 v) {
+    float inv = 1.0f / sqrtf(dot3(v, v));
+    return muls(v, inv);
+}
+__device__ __forceinline__ float length3(f3 v) { return sqrtf(dot3(v, v)); }
+// GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
+__device__ __forceinline__ f3 reflect3(f3 I, f3 N) {
+    float k = 2.0f * dot3(N, I);
+    return sub(I, muls(N, k));
+}
+__device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+
+// ---- primitives (shader.comp line refs) -------------------------------------------------
+
+// ray_aabb_intersect, shader.comp:197-207
+__device__ __forceinline__ bool aabb_hit(f3 o, f3 inv, const float* bmin, const float* bmax) {
+    float t0x = (bmin[0] - o.x) * inv.x, t0y = (bmin[1] - o.y) * inv.y, t0z = (bmin[2] - o.z) * inv.z;
+    float t1x = (bmax[0] - o.x) * inv.x, t1y = (bmax[1] - o.y) * inv.y, t1z = (bmax[2] - o.z) * inv.z;
+    float tNear = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    float tFar = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    return tNear <= tFar && tFar > TRT_EPS;
+}
+
+// ray_sphere_intersect, shader.comp:272-285
+__device__ __forceinline__ bool sphere_hit(f3 o, f3 d, const SphereArg& s, float& t) {
+    f3 L = sub(mk(s.c[0], s.c[1], s.c[2]), o);
+    float tca = dot3(L, d);
+    float d2 = dot3(L, L) - tca * tca;
+    float r2 = s.r * s.r;
+    if (d2 > r2) return false;
+    float thc = sqrtf(r2 - d2);
+    float t0 = tca - thc, t1 = tca + thc;
+    if (t0 > TRT_EPS) t = t0;
+    else if (t1 > TRT_EPS) t = t1;
+    else return false;
+    return true;
+}
+
+// custom_refract, shader.comp:209-221, called with eta_in = air (1.0)
+__device__ __forceinline__ f3 custom_refract(f3 I, f3 N, float eta_out, float eta_in) {
+    bool entering = dot3(I, N) < 0.0f;
+    f3 fn = entering ? N : neg(N);
+    float cosi = clamp01(dot3(neg(I), fn));
+    float eta = entering ? eta_in / eta_out : eta_out / eta_in;
+    float sint2 = eta * eta * (1.0f - cosi * cosi);
+    if (sint2 > 1.0f) return mk(0.0f, 0.0f, 0.0f);
+    float k = sqrtf(1.0f - sint2);
+    f3 r = add(muls(I, eta), muls(fn, eta * cosi - k));
+    return normalize3(r);
+}
+
+// ---- nearest hit (scene_intersect, shader.comp:295-362) ----------------------------------
+
+enum : int { HIT_NONE = 0, HIT_FLOOR = 1, HIT_SPHERE = 2, HIT_TRI = 3 };
+
+// Per-lane work counters (COUNT builds only): the units of trt_stats.
+struct Cnt {
+    uint32_t pri = 0, sec = 0, sh = 0, miss = 0, trin = 0, sph = 0, bt = 0, bh = 0, tt = 0;
+};
+
+struct Hit {
+    float t;
+    int kind;
+    int idx; // sphere index or triangle index
+    float u, v;
+    int ni; // normal interpolation flag of the batch that produced the triangle hit
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit& h, Cnt& c) {
+    h.t = 1e10f;
+    h.kind = HIT_NONE;
+    h.idx = 0;
+    h.u = 0.0f;
+    h.v = 0.0f;
+    h.ni = 0;
+    if (A.flags & TRT_FLAG_FLOOR) { // shader.comp:302-320
+        if (fabsf(d.y) > TRT_EPS) {
+            float t = -(o.y + 4.0f) / d.y;
+            if (t > TRT_EPS && t < h.t) {
+                f3 p = add(o, muls(d, t));
+                if (fabsf(p.x) < 10.0f && p.z < -5.0f && p.z > -30.0f) {
+                    h.t = t;
+                    h.kind = HIT_FLOOR;
+                }
+            }
+        }
+    }
+    if (A.flags & TRT_FLAG_SPHERES) { // shader.comp:322-335
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float t = 1e10f;
+            if (COUNT) ++c.sph;
+            if (sphere_hit(o, d, A.sph[i], t) && t < h.t) {
+                h.t = t;
+                h.kind = HIT_SPHERE;
+                h.idx = i;
+            }
+        }
+    }
+    const uint32_t nb = A.nbatch;
+    if (nb == 0) return;
+    f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:336
+    for (uint32_t b = 0; b < nb; ++b) {              // shader.comp:338
+        const BatchRec rec = A.batches[b];           // wave-uniform: scalar load
+        bool hitbox = aabb_hit(o, inv, rec.bmin, rec.bmax);
+        if (COUNT) {
+            ++c.bt;
+            c.bh += hitbox ? 1u : 0u;
+        }
+        if (__ballot(hitbox) == 0) continue; // no lane of the wave enters this batch
+        if (hitbox) {
+            const int start = rec.start;
+            const int count = rec.count_ni & 0x7fffffff;
+            const int ni = (rec.count_ni >> 31) & 1;
+            for (int j = start; j < start + count; ++j) { // shader.comp:344-359
+                const TriGeo g = A.geo[j];                  // wave-uniform: scalar loads
+                if (COUNT) ++c.tt;
+                f3 e1 = ld3(g.e1), e2 = ld3(g.e2), v0 = ld3(g.v0);
+                f3 hv = cross3(d, e2);
+                float a = dot3(e1, hv);
+                if (a > -TRT_EPS && a < TRT_EPS) continue;
+                float f = 1.0f / a;
+                f3 s = sub(o, v0);
+                float u = f * dot3(s, hv);
+                if (u < 0.0f || u > 1.0f) continue;
+                f3 q = cross3(s, e1);
+                float v = f * dot3(d, q);
+                if (v < 0.0f || u + v > 1.0f) continue;
+                float t = f * dot3(e2, q);
+                if (t <= TRT_EPS) continue;
+                if (t > TRT_EPS && t < h.t) {
+                    h.t = t;
+                    h.kind = HIT_TRI;
+                    h.idx = j;
+                    h.u = u;
+                    h.v = v;
+                    h.ni = ni;
+                }
+            }
+        }
+    }
+}
+
+// shadow_intersect, shader.comp:364-399: any hit on spheres / triangles; floor excluded.
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, float max_dist, Cnt& c) {
+    if (A.flags & TRT_FLAG_SPHERES) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float t = 1e10f;
+            if (COUNT) ++c.sph;
+            if (sphere_hit(o, d, A.sph[i], t) && t < max_dist) return true;
+        }
+    }
+    const uint32_t nb = A.nbatch;
+    if (nb == 0) return false;
+    f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    bool occluded = false;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const BatchRec rec = A.batches[b];
+        bool hitbox = !occluded && aabb_hit(o, inv, rec.bmin, rec.bmax);
+        if (COUNT && !occluded) {
+            ++c.bt;
+            c.bh += hitbox ? 1u : 0u;
+        }
+        if (__ballot(hitbox) == 0) {
+            if (__ballot(!occluded) == 0) break;
+            continue;
+        }
+        if (hitbox) {
+            const int start = rec.start;
+            const int count = rec.count_ni & 0x7fffffff;
+            for (int j = start; j < start + count; ++j) {
+                const TriGeo g = A.geo[j];
+                if (COUNT) ++c.tt;
+                f3 e1 = ld3(g.e1), e2 = ld3(g.e2), v0 = ld3(g.v0);
+                f3 hv = cross3(d, e2);
+                float a = dot3(e1, hv);
+                if (a > -TRT_EPS && a < TRT_EPS) continue;
+                float f = 1.0f / a;
+                f3 s = sub(o, v0);
+                float u = f * dot3(s, hv);
+                if (u < 0.0f || u > 1.0f) continue;
+                f3 q = cross3(s, e1);
+                float v = f * dot3(d, q);
+                if (v < 0.0f || u + v > 1.0f) continue;
+                float t = f * dot3(e2, q);
+                if (t <= TRT_EPS) continue;
+                if (t > TRT_EPS && t < max_dist) {
+                    occluded = true;
+                    break;
+                }
+            }
+        }
+    }
+    return occluded;
+}
+
+// ---- background (direction_to_uv + texture(), shader.comp:410-416, 455-458) --------------
+
+__device__ __forceinline__ float unorm8(uint32_t c) { return (float)c / 255.0f; }
+
+__device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
+    if (!(A.flags & TRT_FLAG_ENVMAP)) return mk(0.2f, 0.7f, 0.8f); // BACKGROUND_COLOR :77
+    float theta = atan2f(d.z, d.x);
+    float phi = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
+    float u = (theta + TRT_PI) / (2.0f * TRT_PI);
+    float v = phi / TRT_PI;
+    // Sampler: LINEAR, CLAMP_TO_EDGE, level 0 (main.cpp:1091-1106), R8G8B8A8_UNORM.
+    const int W = (int)A.env_w, H = (int)A.env_h;
+    float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
+    if (!(x == x)) x = 0.0f;
+    if (!(y == y)) y = 0.0f;
+    float xf = floorf(x), yf = floorf(y);
+    float a = x - xf, b = y - yf;
+    // clamp in float first so the int conversion is always in range
+    int ix0 = (int)fminf(fmaxf(xf, -1.0f), (float)W);
+    int iy0 = (int)fminf(fmaxf(yf, -1.0f), (float)H);
+    int ix1 = min(max(ix0 + 1, 0), W - 1);
+    int iy1 = min(max(iy0 + 1, 0), H - 1);
+    ix0 = min(max(ix0, 0), W - 1);
+    iy0 = min(max(iy0, 0), H - 1);
+    const uint32_t* row0 = A.env + (size_t)iy0 * (size_t)W;
+    const uint32_t* row1 = A.env + (size_t)iy1 * (size_t)W;
+    uint32_t c00 = row0[ix0], c10 = row0[ix1], c01 = row1[ix0], c11 = row1[ix1];
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b);
+    float w01 = (1.0f - a) * b, w11 = a * b;
+    float r[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int sh = 8 * k;
+        float t00 = unorm8((c00 >> sh) & 255u), t10 = unorm8((c10 >> sh) & 255u);
+        float t01 = unorm8((c01 >> sh) & 255u), t11 = unorm8((c11 >> sh) & 255u);
+        r[k] = ((w00 * t00 + w10 * t10) + w01 * t01) + w11 * t11;
+    }
+    return mk(r[0], r[1], r[2]);
+}
+
+// ---- cast_ray (shader.comp:423-583) --------------------------------------------------------
+
+struct Seg {
+    f3 o, d;
+    float thr; // throughput is (s,s,s): vec3(1) times scalar albedo weights
+    int depth;
+};
+
+// LIFO of deferred refraction children.  CAP <= 4: register shift-stack (static indices
+// only, so nothing spills to scratch); larger CAP: private array.
+template <int CAP, bool REG = (CAP <= 4)>
+struct DeferStack;
+
+template <int CAP>
+struct DeferStack<CAP, true> {
+    Seg s[CAP > 0 ? CAP : 1];
+    int n = 0;
+    __device__ __forceinline__ void push(const Seg& x) {
+#pragma unroll
+        for (int i = (CAP > 0 ? CAP : 1) - 1; i > 0; --i) s[i] = s[i - 1];
+        s[0] = x;
+        ++n;
+    }
+    __device__ __forceinline__ Seg pop() {
+        Seg x = s[0];
+#pragma unroll
+        for (int i = 0; i < (CAP > 0 ? CAP : 1) - 1; ++i) s[i] = s[i + 1];
+        --n;
+        return x;
+    }
+};
+
+template <int CAP>
+struct DeferStack<CAP, false> {
+    Seg s[CAP];
+    int n = 0;
+    __device__ __forceinline__ void push(const Seg& x) { s[n++] = x; }
+    __device__ __forceinline__ Seg pop() { return s[--n]; }
+};
+
+template <int CAP, bool COUNT>
+__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt) {
+    const int D = (int)A.max_depth;
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    DeferStack<CAP> stk;
+    Seg cur{orig, dir, 1.0f, 0};
+    for (;;) {
+        if (COUNT && cur.depth > 0) ++cnt.sec;
+        Hit h;
+        scene_intersect<COUNT>(A, cur.o, cur.d, h, cnt);
+        bool have_next = false;
+        Seg next;
+        if (h.kind == HIT_NONE) {
+            if (COUNT) ++cnt.miss;
+            f3 bg = background(A, cur.d);
+            color = add(color, muls(bg, cur.thr));
+        } else {
+            // Resolve the closest hit: point, normal, material (shader.comp:302-360).
+            f3 p = add(cur.o, muls(cur.d, h.t));
+            f3 n;
+            float alb[4], kd[3], sexp, ior;
+            if (h.kind == HIT_FLOOR) {
+                n = mk(0.0f, 1.0f, 0.0f);
+                float c0 = 0.3f, c1 = 0.3f, c2 = 0.3f;
+                if (A.flags & TRT_FLAG_CHECKER) { // shader.comp:312
+                    float m = floorf(p.x * 0.5f + 1024.0f) + floorf(p.z * 0.5f);
+                    float mod2 = m - 2.0f * floorf(m / 2.0f);
+                    if (!(mod2 == 0.0f)) {
+                        c1 = 0.2f;
+                        c2 = 0.1f;
+                    }
+                }
+                alb[0] = 2.0f; alb[1] = 0.0f; alb[2] = 0.0f; alb[3] = 0.0f;
+                kd[0] = c0; kd[1] = c1; kd[2] = c2;
+                sexp = 1.0f;
+                ior = 1.0f;
+            } else if (h.kind == HIT_SPHERE) {
+                const SphereArg& s = A.sph[h.idx];
+                n = normalize3(sub(p, mk(s.c[0], s.c[1], s.c[2])));
+#pragma unroll
+                for (int k = 0; k < 4; ++k) alb[k] = s.m.albedo[k];
+                kd[0] = s.m.kd[0]; kd[1] = s.m.kd[1]; kd[2] = s.m.kd[2];
+                sexp = s.m.spec_exp;
+                ior = s.m.ior;
+            } else {
+                if (COUNT) ++cnt.trin;
+                const TriShade& ts = A.shade[h.idx];
+                if (h.ni == 0) {
+                    const TriGeo& g = A.geo[h.idx];
+                    n = normalize3(cross3(ld3(g.e1), ld3(g.e2)));
+                } else {
+                    float w = 1.0f - h.u - h.v;
+                    f3 nn = add(add(muls(ld3(ts.n0), w), muls(ld3(ts.n1), h.u)), muls(ld3(ts.n2), h.v));
+                    n = normalize3(nn);
+                }
+                const Mat& m = A.mats[ts.material];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) alb[k] = m.albedo[k];
+                kd[0] = m.kd[0]; kd[1] = m.kd[1]; kd[2] = m.kd[2];
+                sexp = m.spec_exp;
+                ior = m.ior;
+            }
+            // Phong with three shadow rays, shader.comp:483-507.
+            f3 v = neg(cur.d);
+            f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
+            f3 kdv = mk(kd[0], kd[1], kd[2]);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
+                f3 ld = normalize3(sub(L, p));
+                float dist = length3(sub(L, p));
+                f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
+                if (COUNT) ++cnt.sh;
+                if (shadow_intersect<COUNT>(A, so, ld, dist, cnt)) continue;
+                float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
+                diffuse = add(diffuse, muls(kdv, diff));
+                f3 rdir = reflect3(neg(ld), n);
+                float spec = 1.0f * powf(fmaxf(0.0f, dot3(rdir, v)), sexp);
+                specular = add(specular, muls(kdv, spec));
+            }
+            color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
+            // Children (shader.comp:509-575).  Children that the reference would push and
+            // then drop unseen at the depth / throughput test (shader.comp:449) are not made.
+            const int cd = cur.depth + 1;
+            bool mk_refr = false, mk_refl = false;
+            Seg refr, refl;
+            bool skip_reflect = false;
+            if (alb[3] > 0.0f) {
+                f3 rd = custom_refract(cur.d, n, ior, 1.0f);
+                if (length3(rd) > 0.0001f) {
+                    rd = normalize3(rd);
+                } else { // total internal reflection: one reflected child, shader.comp:533-555
+                    rd = normalize3(reflect3(cur.d, n));
+                    skip_reflect = true;
+                }
+                f3 off = dot3(rd, n) < 0.0f ? muls(neg(n), TRT_EPS) : muls(n, TRT_EPS);
+                refr = Seg{add(p, off), rd, cur.thr * alb[3], cd};
+                float tt = (refr.thr * refr.thr + refr.thr * refr.thr) + refr.thr * refr.thr;
+                mk_refr = cd < D && !(tt < 0.001f);
+            }
+            if (alb[2] > 0.0f && !skip_reflect) {
+                f3 rd = normalize3(reflect3(cur.d, n));
+                f3 off = dot3(rd, n) < 0.0f ? muls(neg(n), TRT_EPS) : muls(n, TRT_EPS);
+                refl = Seg{add(p, off), rd, cur.thr * alb[2], cd};
+                float tt = (refl.thr * refl.thr + refl.thr * refl.thr) + refl.thr * refl.thr;
+                mk_refl = cd < D && !(tt < 0.001f);
+            }
+            // Reference pushes refraction then reflection and pops reflection first.
+            if (mk_refl) {
+                if (mk_refr) stk.push(refr);
+                next = refl;
+                have_next = true;
+            } else if (mk_refr) {
+                next = refr;
+                have_next = true;
+            }
+        }
+        if (have_next) {
+            cur = next;
+        } else if (stk.n > 0) {
+            cur = stk.pop();
+        } else {
+            break;
+        }
+    }
+    return mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)); // shader.comp:582
+}
+
+// ---- primary rays (main.cpp:1496-1506 on the host; shader.comp:592-595) -----------------
+
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+
+__device__ __forceinline__ f3 primary_dir(const KArgs& A, uint32_t x, uint32_t y, uint32_t sample) {
+    const uint32_t W = A.width, H = A.height;
+    const uint64_t pix = (uint64_t)y * W + x;
+    f3 d;
+    if (A.rays_in) {
+        const float* r = A.rays_in + 8 * pix; // Ray.dir (binding 1)
+        d = mk(r[0], r[1], r[2]);
+    } else {
+        const uint64_t row = (A.flags & TRT_FLAG_ROW_QUIRK) ? (pix + 1) / W : y;
+        float dx, dy;
+        if (A.spp <= 1) { // exact in float: half-integers (main.cpp:1501-1502)
+            dx = ((float)x + 0.5f) - (float)W * 0.5f;
+            dy = -((float)row + 0.5f) + (float)H * 0.5f;
+        } else {
+            uint32_t k = pcg_hash(A.seed ^ 0x9E3779B9u);
+            uint32_t a = pcg_hash(k + (uint32_t)pix);
+            uint32_t b = pcg_hash(a + sample);
+            uint32_t c = pcg_hash(b);
+            float jx = (float)(b >> 8) * (1.0f / 16777216.0f);
+            float jy = (float)(c >> 8) * (1.0f / 16777216.0f);
+            dx = ((float)x + jx) - (float)W * 0.5f;
+            dy = (float)H * 0.5f - ((float)row + jy);
+        }
+        d = normalize3(mk(dx, dy, A.dz)); // glm::normalize, main.cpp:1504
+    }
+    return normalize3(d); // shader.comp:593
+}
+
+// ---- the kernel ------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t band_row(const KArgs& A, uint32_t k) {
+    if (A.band_rows == 0 || A.band_count <= 1) return k;
+    const uint32_t B = A.band_rows;
+    return ((k / B) * A.band_count + A.band_index) * B + (k % B);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+template <int CAP, bool COUNT>
+__global__ __launch_bounds__(256) void trace_kernel(KArgs A) {
+    // 16x16 pixel tile per workgroup, 8x8 per wave.
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t k = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    Cnt cnt;
+    if (x < A.width && k < A.rows) {
+        const uint32_t y = band_row(A, k);
+        const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
+        const uint32_t spp = A.spp ? A.spp : 1u;
+        f3 acc = mk(0.0f, 0.0f, 0.0f);
+        for (uint32_t s = 0; s < spp; ++s) {
+            f3 d = primary_dir(A, x, y, s);
+            f3 c = cast_ray<CAP, COUNT>(A, orig, d, cnt);
+            acc = (spp == 1u) ? c : add(acc, c);
+        }
+        cnt.pri = spp;
+        if (spp > 1u) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
+        // pow(color, vec3(GAMMA)), shader.comp:598
+        const float gx = powf(acc.x, TRT_GAMMA), gy = powf(acc.y, TRT_GAMMA), gz = powf(acc.z, TRT_GAMMA);
+        const size_t o = (size_t)k * A.width + x;
+        if (A.out32) { // rayOut[idx].resultColor, shader.comp:601
+            reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
+        }
+        if (A.out8) { // rgba8 storage image, shader.comp:61, 600
+            uint32_t r = (uint32_t)floorf(gx * 255.0f + 0.5f);
+            uint32_t g = (uint32_t)floorf(gy * 255.0f + 0.5f);
+            uint32_t b = (uint32_t)floorf(gz * 255.0f + 0.5f);
+            A.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
+        }
+    }
+    if (COUNT) {
+        const uint32_t v[9] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt};
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            unsigned long long w = wave_sum((unsigned long long)v[i]);
+            if (lane == 0) atomicAdd(&A.counters[i], w);
+        }
+    }
+}
+
+// Launch helper: picks the deferred-stack capacity from max_depth (children are made only
+// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once).
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
+    dim3 block(256);
+    dim3 grid((A.width + 15u) / 16u, (A.rows + 15u) / 16u);
+    const uint32_t D = A.max_depth;
+#define TRT_LAUNCH(CAP)                                                              \
+    do {                                                                             \
+        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true>), grid, block, 0, stream, A);  \
+        else hipLaunchKernelGGL((trace_kernel<CAP, false>), grid, block, 0, stream, A);       \
+    } while (0)
+    if (D <= 1) TRT_LAUNCH(0);
+    else if (D <= 2) TRT_LAUNCH(1);
+    else if (D <= 3) TRT_LAUNCH(2);
+    else if (D <= 4) TRT_LAUNCH(3);
+    else if (D <= 5) TRT_LAUNCH(4);
+    else if (D <= 8) TRT_LAUNCH(7);
+    else TRT_LAUNCH(19);
+#undef TRT_LAUNCH
+    return hipGetLastError();
+}
+
+} // namespace trt

@@ -1,0 +1,443 @@
+// trt_runtime.cpp — the C-ABI (include/trt/abi.h) over the HIP runtime.
+//
+// Replaces the reference's Vulkan compute plumbing: createShaderStorageBuffers() /
+// createUniformBuffers() / the background texture upload (main.cpp:928-1111, 1494-1664)
+// become trt_upload_scene(); updateUniformBuffer() (main.cpp:2165-2179) becomes
+// trt_update_ubo(); recordComputeCommandBuffer() + vkQueueSubmit (main.cpp:2108-2131,
+// 2181-2205) become trt_render().  No exception crosses the ABI; failures set the context's
+// last error and return a negative TRT_ERR_* code (the reference throws std::runtime_error
+// and exits, main.cpp:2565-2573).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/trt/abi.h"
+#include "trt_device.h"
+
+namespace trt {
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
+}
+
+using trt::BatchRec;
+using trt::KArgs;
+using trt::Mat;
+using trt::TriGeo;
+using trt::TriShade;
+
+struct trt_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    trt_ubo ubo{};
+    bool have_scene = false;
+
+    BatchRec* d_batches = nullptr;
+    TriGeo* d_geo = nullptr;
+    TriShade* d_shade = nullptr;
+    Mat* d_mats = nullptr;
+    uint32_t* d_env = nullptr;
+    uint32_t nbatch = 0, ntri = 0, nmat = 0, env_w = 0, env_h = 0;
+
+    void* d_out8 = nullptr;
+    size_t cap8 = 0;
+    void* d_out32 = nullptr;
+    size_t cap32 = 0;
+    void* d_rays = nullptr;
+    size_t caprays = 0;
+    unsigned long long* d_counters = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+int fail(trt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(trt_ctx* c, hipError_t e, const char* what) {
+    return fail(c, TRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr)                                       \
+    do {                                                         \
+        hipError_t e_ = (expr);                                  \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr); \
+    } while (0)
+
+void free_scene(trt_ctx* c) {
+    (void)hipFree(c->d_batches);
+    (void)hipFree(c->d_geo);
+    (void)hipFree(c->d_shade);
+    (void)hipFree(c->d_mats);
+    (void)hipFree(c->d_env);
+    c->d_batches = nullptr;
+    c->d_geo = nullptr;
+    c->d_shade = nullptr;
+    c->d_mats = nullptr;
+    c->d_env = nullptr;
+    c->nbatch = c->ntri = c->nmat = c->env_w = c->env_h = 0;
+    c->have_scene = false;
+}
+
+// Grow-only device scratch buffer.
+int ensure(trt_ctx* c, void** p, size_t* cap, size_t bytes, const char* what) {
+    if (bytes <= *cap && *p) return TRT_OK;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return hip_fail(c, e, what);
+    *cap = bytes;
+    return TRT_OK;
+}
+
+Mat to_mat(const trt_material& m) {
+    Mat r{};
+    r.albedo[0] = m.albedo.x;
+    r.albedo[1] = m.albedo.y;
+    r.albedo[2] = m.albedo.z;
+    r.albedo[3] = m.albedo.w;
+    r.kd[0] = m.diffuse_specular.x;
+    r.kd[1] = m.diffuse_specular.y;
+    r.kd[2] = m.diffuse_specular.z;
+    r.spec_exp = m.diffuse_specular.w;
+    r.ior = m.refractive.x;
+    return r;
+}
+
+void fill_ubo_args(KArgs& A, const trt_ubo& u) {
+    const trt_sphere* s[4] = {&u.sphere0, &u.sphere1, &u.sphere2, &u.sphere3};
+    for (int i = 0; i < 4; ++i) {
+        A.sph[i].c[0] = s[i]->center_radius.x;
+        A.sph[i].c[1] = s[i]->center_radius.y;
+        A.sph[i].c[2] = s[i]->center_radius.z;
+        A.sph[i].r = s[i]->center_radius.w;
+        A.sph[i].m = to_mat(s[i]->material);
+    }
+    const trt_vec4* l[3] = {&u.light0, &u.light1, &u.light2};
+    for (int i = 0; i < 3; ++i) {
+        A.light[i][0] = l[i]->x;
+        A.light[i][1] = l[i]->y;
+        A.light[i][2] = l[i]->z;
+    }
+    A.cam[0] = u.camPos.x;
+    A.cam[1] = u.camPos.y;
+    A.cam[2] = u.camPos.z;
+}
+
+bool row_selected(const trt_params* p, uint32_t r) {
+    if (p->band_rows == 0 || p->band_count <= 1) return true;
+    return (r / p->band_rows) % p->band_count == p->band_index;
+}
+
+} // namespace
+
+extern "C" {
+
+const char* trt_version(void) { return "trt-mi355x 0.1 (gfx950, abi 1)"; }
+
+void trt_params_default(trt_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->width = 1024;  // main.cpp:35
+    p->height = 768;  // main.cpp:36
+    p->max_depth = 20; // shader.comp:75
+    p->spp = 1;
+    p->fov = 1.05f; // main.cpp:1498
+    p->flags = TRT_FLAGS_REFERENCE;
+}
+
+uint32_t trt_output_rows(const trt_params* p) {
+    if (!p) return 0;
+    if (p->band_rows == 0 || p->band_count <= 1) return p->height;
+    uint32_t n = 0;
+    for (uint32_t r = 0; r < p->height; ++r) n += row_selected(p, r) ? 1u : 0u;
+    return n;
+}
+
+int trt_create(trt_ctx** out, int hip_device) {
+    if (!out) return TRT_ERR_INVALID;
+    *out = nullptr;
+    trt_ctx* c = new (std::nothrow) trt_ctx();
+    if (!c) return TRT_ERR_OOM;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0 || hip_device < 0 || hip_device >= n) {
+        delete c;
+        return TRT_ERR_HIP;
+    }
+    c->device = hip_device;
+    if (hipSetDevice(hip_device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        trt_destroy(c);
+        return TRT_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return TRT_OK;
+}
+
+int trt_destroy(trt_ctx* c) {
+    if (!c) return TRT_ERR_INVALID;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    (void)hipFree(c->d_out8);
+    (void)hipFree(c->d_out32);
+    (void)hipFree(c->d_rays);
+    (void)hipFree(c->d_counters);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return TRT_OK;
+}
+
+const char* trt_last_error(const trt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int trt_set_stream(trt_ctx* c, void* s) {
+    if (!c) return TRT_ERR_INVALID;
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    return TRT_OK;
+}
+
+int trt_synchronize(trt_ctx* c) {
+    if (!c) return TRT_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return TRT_OK;
+}
+
+int trt_update_ubo(trt_ctx* c, const trt_ubo* ubo) {
+    if (!c || !ubo) return fail(c, TRT_ERR_INVALID, "trt_update_ubo: null argument");
+    c->ubo = *ubo;
+    return TRT_OK;
+}
+
+int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, uint32_t ntri,
+                     const trt_model* models, uint32_t nmodel, const uint8_t* env,
+                     uint32_t env_w, uint32_t env_h) {
+    if (!c) return TRT_ERR_INVALID;
+    if (!ubo) return fail(c, TRT_ERR_INVALID, "trt_upload_scene: null ubo");
+    if (ntri && !tris) return fail(c, TRT_ERR_INVALID, "trt_upload_scene: null triangles");
+    if (nmodel && !models) return fail(c, TRT_ERR_INVALID, "trt_upload_scene: null models");
+    if (env && (env_w == 0 || env_h == 0))
+        return fail(c, TRT_ERR_INVALID, "trt_upload_scene: zero-size envmap");
+    for (uint32_t i = 0; i < nmodel; ++i) {
+        const int64_t s = models[i].params0.x, n = models[i].params0.y;
+        if (s < 0 || n < 0 || s + n > (int64_t)ntri)
+            return fail(c, TRT_ERR_INVALID,
+                        "trt_upload_scene: model " + std::to_string(i) +
+                            " triangle range outside the triangle buffer");
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    free_scene(c);
+
+    // Repack binding 6 (Model) and binding 5 (Triangle) for the wave-uniform walks.
+    std::vector<BatchRec> batches(nmodel);
+    for (uint32_t i = 0; i < nmodel; ++i) {
+        const trt_model& m = models[i];
+        BatchRec& b = batches[i];
+        b.bmin[0] = m.bboxMin.x;
+        b.bmin[1] = m.bboxMin.y;
+        b.bmin[2] = m.bboxMin.z;
+        b.bmax[0] = m.bboxMax.x;
+        b.bmax[1] = m.bboxMax.y;
+        b.bmax[2] = m.bboxMax.z;
+        b.start = m.params0.x;
+        b.count_ni = (m.params0.y & 0x7fffffff) | (m.params0.z != 0 ? (int32_t)0x80000000 : 0);
+    }
+    std::vector<TriGeo> geo(ntri);
+    std::vector<TriShade> shade(ntri);
+    std::vector<Mat> mats;
+    std::map<std::string, uint32_t> mat_index;
+    for (uint32_t j = 0; j < ntri; ++j) {
+        const trt_triangle& t = tris[j];
+        TriGeo& g = geo[j];
+        g.v0[0] = t.v0.x;
+        g.v0[1] = t.v0.y;
+        g.v0[2] = t.v0.z;
+        // edge1 = v1 - v0, edge2 = v2 - v0 (shader.comp:230-231): same float subtraction
+        g.e1[0] = t.v1.x - t.v0.x;
+        g.e1[1] = t.v1.y - t.v0.y;
+        g.e1[2] = t.v1.z - t.v0.z;
+        g.e2[0] = t.v2.x - t.v0.x;
+        g.e2[1] = t.v2.y - t.v0.y;
+        g.e2[2] = t.v2.z - t.v0.z;
+        g.pad[0] = g.pad[1] = g.pad[2] = 0.0f;
+        TriShade& s = shade[j];
+        s.n0[0] = t.v0_norm.x;
+        s.n0[1] = t.v0_norm.y;
+        s.n0[2] = t.v0_norm.z;
+        s.n1[0] = t.v1_norm.x;
+        s.n1[1] = t.v1_norm.y;
+        s.n1[2] = t.v1_norm.z;
+        s.n2[0] = t.v2_norm.x;
+        s.n2[1] = t.v2_norm.y;
+        s.n2[2] = t.v2_norm.z;
+        std::string key(reinterpret_cast<const char*>(&t.material), sizeof(trt_material));
+        auto it = mat_index.find(key);
+        if (it == mat_index.end()) {
+            it = mat_index.emplace(key, (uint32_t)mats.size()).first;
+            mats.push_back(to_mat(t.material));
+        }
+        s.material = it->second;
+        s.pad[0] = s.pad[1] = 0;
+    }
+    if (mats.empty()) mats.push_back(Mat{});
+
+    auto upload = [&](void** dst, const void* src, size_t bytes, const char* what) -> int {
+        if (bytes == 0) bytes = 16; // never bind a null buffer
+        hipError_t e = hipMalloc(dst, bytes);
+        if (e != hipSuccess) return hip_fail(c, e, what);
+        if (src) {
+            e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+            if (e != hipSuccess) return hip_fail(c, e, what);
+        }
+        return TRT_OK;
+    };
+    int rc;
+    if ((rc = upload((void**)&c->d_batches, nmodel ? batches.data() : nullptr,
+                     sizeof(BatchRec) * nmodel, "upload batches")) != TRT_OK ||
+        (rc = upload((void**)&c->d_geo, ntri ? geo.data() : nullptr, sizeof(TriGeo) * ntri,
+                     "upload triangle geometry")) != TRT_OK ||
+        (rc = upload((void**)&c->d_shade, ntri ? shade.data() : nullptr, sizeof(TriShade) * ntri,
+                     "upload triangle shading")) != TRT_OK ||
+        (rc = upload((void**)&c->d_mats, mats.data(), sizeof(Mat) * mats.size(),
+                     "upload materials")) != TRT_OK) {
+        free_scene(c);
+        return rc;
+    }
+    if (env) {
+        if ((rc = upload((void**)&c->d_env, env, (size_t)env_w * env_h * 4, "upload envmap")) != TRT_OK) {
+            free_scene(c);
+            return rc;
+        }
+        c->env_w = env_w;
+        c->env_h = env_h;
+    }
+    c->nbatch = nmodel;
+    c->ntri = ntri;
+    c->nmat = (uint32_t)mats.size();
+    c->ubo = *ubo;
+    c->have_scene = true;
+    return TRT_OK;
+}
+
+int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt_stats* st) {
+    if (!c) return TRT_ERR_INVALID;
+    if (!p) return fail(c, TRT_ERR_INVALID, "trt_render: null params");
+    if (!c->have_scene) return fail(c, TRT_ERR_NOSCENE, "trt_render: no scene uploaded");
+    if (p->width == 0 || p->height == 0 || p->width > 65536 || p->height > 65536)
+        return fail(c, TRT_ERR_INVALID, "trt_render: image size out of range");
+    if (p->max_depth < 1 || p->max_depth > TRT_MAX_DEPTH_LIMIT)
+        return fail(c, TRT_ERR_INVALID, "trt_render: max_depth must be 1..20");
+    if (p->spp > 4096) return fail(c, TRT_ERR_INVALID, "trt_render: spp must be <= 4096");
+    if (p->band_rows && p->band_count > 1 && p->band_index >= p->band_count)
+        return fail(c, TRT_ERR_INVALID, "trt_render: band_index >= band_count");
+    if ((p->flags & TRT_FLAG_ENVMAP) && !c->d_env)
+        return fail(c, TRT_ERR_INVALID, "trt_render: TRT_FLAG_ENVMAP without an uploaded envmap");
+    HIP_TRY(c, hipSetDevice(c->device));
+
+    const bool dev = (p->flags & TRT_FLAG_DEVICE_PTRS) != 0;
+    const bool count = (p->flags & TRT_FLAG_COUNT) != 0 && st;
+    const bool timing = (p->flags & TRT_FLAG_TIMING) != 0 && st;
+    const uint32_t rows = trt_output_rows(p);
+    const size_t npx = (size_t)rows * p->width;
+
+    KArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.width = p->width;
+    A.height = p->height;
+    A.rows = rows;
+    A.band_rows = p->band_rows;
+    A.band_count = p->band_count;
+    A.band_index = p->band_index;
+    A.max_depth = p->max_depth;
+    A.spp = p->spp ? p->spp : 1;
+    A.seed = p->seed;
+    A.flags = p->flags;
+    // dir_z = -1.0 * (HEIGHT / (2.0 * tan(fov / 2.0))) in double, main.cpp:1503
+    A.dz = (float)(-1.0 * ((double)p->height / (2.0 * std::tan((double)p->fov / 2.0))));
+    A.nbatch = c->nbatch;
+    fill_ubo_args(A, c->ubo);
+    A.batches = c->d_batches;
+    A.geo = c->d_geo;
+    A.shade = c->d_shade;
+    A.mats = c->d_mats;
+    A.env = c->d_env;
+    A.env_w = c->env_w;
+    A.env_h = c->env_h;
+    A.counters = c->d_counters;
+
+    int rc;
+    if (p->rays_in) {
+        if (dev) {
+            A.rays_in = reinterpret_cast<const float*>(p->rays_in);
+        } else {
+            const size_t bytes = sizeof(trt_ray) * (size_t)p->width * p->height;
+            if ((rc = ensure(c, &c->d_rays, &c->caprays, bytes, "alloc rays")) != TRT_OK) return rc;
+            HIP_TRY(c, hipMemcpyAsync(c->d_rays, p->rays_in, bytes, hipMemcpyHostToDevice, c->stream));
+            A.rays_in = reinterpret_cast<const float*>(c->d_rays);
+        }
+    }
+    if (out8) {
+        if (dev) {
+            A.out8 = reinterpret_cast<uint32_t*>(out8);
+        } else {
+            if ((rc = ensure(c, &c->d_out8, &c->cap8, npx * 4, "alloc rgba8")) != TRT_OK) return rc;
+            A.out8 = reinterpret_cast<uint32_t*>(c->d_out8);
+        }
+    }
+    if (out32) {
+        if (dev) {
+            A.out32 = out32;
+        } else {
+            if ((rc = ensure(c, &c->d_out32, &c->cap32, npx * 16, "alloc rgba32f")) != TRT_OK) return rc;
+            A.out32 = reinterpret_cast<float*>(c->d_out32);
+        }
+    }
+    if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
+    if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+    if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
+    if (timing) HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+    if (out8 && !dev)
+        HIP_TRY(c, hipMemcpyAsync(out8, c->d_out8, npx * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out32 && !dev)
+        HIP_TRY(c, hipMemcpyAsync(out32, c->d_out32, npx * 16, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long cnt[16] = {0};
+    if (count)
+        HIP_TRY(c, hipMemcpyAsync(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    if (!dev || count || timing) HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (st) {
+        st->primary_rays = cnt[0];
+        st->secondary_rays = cnt[1];
+        st->shadow_rays = cnt[2];
+        st->misses = cnt[3];
+        st->tri_nearest = cnt[4];
+        st->sphere_tests = cnt[5];
+        st->batch_tests = cnt[6];
+        st->batch_hits = cnt[7];
+        st->tri_tests = cnt[8];
+        st->kernel_ms = 0.0;
+        if (timing) {
+            float ms = 0.0f;
+            HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+            st->kernel_ms = ms;
+        }
+    }
+    return TRT_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,133 @@
+"""Host-side mirror of the reference's compute path, over the C-ABI.
+
+The reference's ComputeShaderApplication drives the hot path as
+  createShaderStorageBuffers() + createUniformBuffers()  -> Renderer.upload_scene()
+  updateUniformBuffer()                                  -> Renderer.update_ubo()
+  recordComputeCommandBuffer() + vkQueueSubmit()         -> Renderer.draw_frame()
+(main.cpp:1494-1664, 2108-2205).  Output pointers may be numpy arrays (host) or torch CUDA
+tensors (device, rendered in place on the context's stream).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import types as T
+from ._lib import TrtError, lib
+from .scene import Scene
+
+
+def _is_torch_cuda(x) -> bool:
+    return hasattr(x, "is_cuda") and bool(x.is_cuda)
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        rc = self._L.trt_create(ctypes.byref(h), int(device))
+        if rc != 0:
+            raise TrtError(rc, f"trt_create(device={device}) failed: no usable HIP device")
+        self._h = h
+        self.device = device
+        self.scene: Scene | None = None
+
+    # -- errors ----------------------------------------------------------------------------
+    def _check(self, rc: int):
+        if rc != 0:
+            raise TrtError(rc, self._L.trt_last_error(self._h).decode())
+
+    # -- bindings --------------------------------------------------------------------------
+    def upload_scene(self, scene: Scene) -> None:
+        ubo = np.ascontiguousarray(scene.ubo)
+        tris = np.ascontiguousarray(scene.tris, T.TRIANGLE)
+        models = np.ascontiguousarray(scene.models, T.MODEL)
+        env = None if scene.env is None else np.ascontiguousarray(scene.env, np.uint8)
+        self._check(self._L.trt_upload_scene(
+            self._h, ubo.ctypes.data, tris.ctypes.data if len(tris) else None, len(tris),
+            models.ctypes.data if len(models) else None, len(models),
+            env.ctypes.data if env is not None else None,
+            0 if env is None else env.shape[1], 0 if env is None else env.shape[0]))
+        self.scene = scene
+
+    def update_ubo(self, ubo: np.ndarray) -> None:
+        u = np.ascontiguousarray(ubo)
+        self._check(self._L.trt_update_ubo(self._h, u.ctypes.data))
+
+    def set_stream(self, stream) -> None:
+        """`stream`: a torch.cuda.Stream, a raw hipStream_t int, or None (own stream)."""
+        s = getattr(stream, "cuda_stream", stream)
+        self._check(self._L.trt_set_stream(self._h, ctypes.c_void_p(s) if s else None))
+
+    def synchronize(self) -> None:
+        self._check(self._L.trt_synchronize(self._h))
+
+    # -- frames ----------------------------------------------------------------------------
+    def draw_frame(self, params: T.Params, out8=None, out32=None, rays_in=None, count: bool = False,
+                   timing: bool = False, want8: bool = True, want32: bool = False):
+        """Renders one frame.  With numpy/None outputs returns host arrays
+        (rows, W, 4) uint8 / float32; with torch CUDA tensors renders into them in place.
+        Returns (rgba8, rgba32f, stats_dict)."""
+        p = T.Params.from_buffer_copy(params)
+        rows = int(self._L.trt_output_rows(ctypes.byref(p)))
+        dev = _is_torch_cuda(out8) or _is_torch_cuda(out32) or _is_torch_cuda(rays_in)
+        if dev:
+            p.flags |= T.FLAG_DEVICE_PTRS
+            for x in (out8, out32, rays_in):
+                if x is not None and not _is_torch_cuda(x):
+                    raise ValueError("mixing host and device pointers in one draw_frame call")
+            if out8 is not None:
+                assert out8.is_contiguous() and out8.numel() >= rows * p.width * 4
+            if out32 is not None:
+                assert out32.is_contiguous() and out32.numel() >= rows * p.width * 4
+            o8 = out8.data_ptr() if out8 is not None else None
+            o32 = out32.data_ptr() if out32 is not None else None
+            if rays_in is not None:
+                p.rays_in = rays_in.data_ptr()
+        else:
+            if out8 is None and want8:
+                out8 = np.empty((rows, p.width, 4), np.uint8)
+            if out32 is None and want32:
+                out32 = np.empty((rows, p.width, 4), np.float32)
+            if out8 is not None:
+                assert out8.flags["C_CONTIGUOUS"] and out8.size >= rows * p.width * 4
+            if out32 is not None:
+                assert out32.flags["C_CONTIGUOUS"] and out32.size >= rows * p.width * 4
+            o8 = out8.ctypes.data if out8 is not None else None
+            o32 = out32.ctypes.data if out32 is not None else None
+            if rays_in is not None:
+                rays_in = np.ascontiguousarray(rays_in, T.RAY)
+                assert rays_in.size >= p.width * p.height
+                p.rays_in = rays_in.ctypes.data
+        if count:
+            p.flags |= T.FLAG_COUNT
+        if timing:
+            p.flags |= T.FLAG_TIMING
+        st = T.Stats()
+        self._check(self._L.trt_render(self._h, ctypes.byref(p), o8, o32, ctypes.byref(st)))
+        return out8, out32, st.as_dict()
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.trt_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render(scene: Scene, device: int = 0, **kw):
+    """One-shot convenience: upload + one frame with the scene's own settings."""
+    with Renderer(device) as r:
+        r.upload_scene(scene)
+        return r.draw_frame(scene.params(), **kw)
