@@ -121,38 +121,33 @@ def main():
 
     r = trt.Renderer(dev)
     r.upload_scene(scene)
-    stream = torch.cuda.current_stream()
-    r.set_stream(stream)
     out8 = torch.empty((rows, params.width, 4), dtype=torch.uint8, device="cuda")
 
     # Counting pass (excluded from timing): rays and per-stage work of this rank's frame.
-    r.set_stream(None)
     _, _, st = r.draw_frame(params, count=True)
-    r.set_stream(stream)
     rays_per_frame = st["primary_rays"] + st["secondary_rays"]
     alg_bytes = algorithmic_bytes(st, pixels, envmap)
 
-    for _ in range(args.warmup):
-        r.draw_frame(params, out8=out8)
+    # Frames are enqueued by the native frame loop (trt_render_frames: one kernel launch per
+    # frame, HIP event pair around each launch on the kernel's own stream).
+    stream = torch.cuda.Stream()
+    r.set_stream(stream)
+    r.render_frames(params, out8, args.warmup)
     torch.cuda.synchronize()
 
     K = args.steps
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        evs[k][0].record(stream)
-        r.draw_frame(params, out8=out8)
-        evs[k][1].record(stream)
+    r.render_frames(params, out8, K, timing=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    kern_ms = r.frame_times(K)
+    kern_avg_ms = float(kern_ms.mean())
 
     total_rays = rays_per_frame
     if dist:

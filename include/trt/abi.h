@@ -96,8 +96,8 @@ int trt_create(trt_ctx** out, int hip_device);
 int trt_destroy(trt_ctx* ctx);
 const char* trt_last_error(const trt_ctx* ctx);
 
-/* Launch subsequent work on an external hipStream_t (e.g. torch's current stream); NULL
- * restores the context's own stream. */
+/* Launch subsequent work on an external hipStream_t (e.g. a torch.cuda.Stream); NULL
+ * restores the context's own stream (the legacy null stream cannot be selected). */
 int trt_set_stream(trt_ctx* ctx, void* hip_stream);
 
 /* Uploads the bindings of one scene.  ntri/nmodel may be 0 (the reference cannot bind a
@@ -116,6 +116,19 @@ int trt_update_ubo(trt_ctx* ctx, const trt_ubo* ubo);
  * pointers and no COUNT/TIMING flag the call only enqueues work on the stream. */
 int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out_rgba32f,
                trt_stats* st);
+
+/* The reference's frame loop (mainLoop -> drawFrame, main.cpp:405-438, 2181-2205) in one
+ * call: for each of `nframes` frames, updateUniformBuffer with ubos[i] (or the current UBO
+ * when ubos is NULL) and enqueue one trace launch writing out_rgba8 + i * frame_stride
+ * bytes (frame_stride 0 = every frame overwrites the same image).  Requires
+ * TRT_FLAG_DEVICE_PTRS; only enqueues.  Host cost per frame is one kernel launch, so
+ * back-to-back frames keep the GPU busy.  With TRT_FLAG_TIMING a HIP event pair brackets
+ * every launch on the stream; trt_frame_times() reads the per-frame kernel times. */
+int trt_render_frames(trt_ctx* ctx, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
+                      uint8_t* out_rgba8, size_t frame_stride);
+
+/* Per-frame device times (ms) of the last timed trt_render_frames call (waits for them). */
+int trt_frame_times(trt_ctx* ctx, float* ms, uint32_t n);
 
 /* Waits for all work enqueued on the context's stream. */
 int trt_synchronize(trt_ctx* ctx);

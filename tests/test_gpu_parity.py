@@ -16,7 +16,7 @@ SMALL_ENV = (1024, 512)
 
 
 def _counts(st):
-    return (st["primary_rays"], st["secondary_rays"], st["shadow_rays"])
+    return tuple(st[k] for k in T.Stats.COUNTERS)
 
 
 def _check(r, sc, params=None, want32=True, max_frac=0.02):
@@ -155,9 +155,12 @@ def test_device_pointers_torch(gpu_renderer):
     host8, host32, _ = gpu_renderer.draw_frame(sc.params(), want32=True)
     out8 = torch.empty((96, 160, 4), dtype=torch.uint8, device="cuda")
     out32 = torch.empty((96, 160, 4), dtype=torch.float32, device="cuda")
-    gpu_renderer.set_stream(torch.cuda.current_stream())
+    stream = torch.cuda.Stream()
+    gpu_renderer.set_stream(stream)
     gpu_renderer.draw_frame(sc.params(), out8=out8, out32=out32)
     torch.cuda.synchronize()
+    with pytest.raises(ValueError):
+        gpu_renderer.set_stream(torch.cuda.default_stream())
     gpu_renderer.set_stream(None)
     assert np.array_equal(out8.cpu().numpy(), host8)
     assert np.array_equal(out32.cpu().numpy(), host32)
@@ -200,3 +203,23 @@ def test_errors(gpu_renderer):
     gpu_renderer.upload_scene(no_env)
     with pytest.raises(TrtError):
         gpu_renderer.draw_frame(no_env.params(width=8, height=8))
+
+
+def test_frame_loop_matches_single_frames(gpu_renderer):
+    """trt_render_frames (native frame loop with per-frame UBOs) == trt_render per frame."""
+    torch = pytest.importorskip("torch")
+    sc = S.config_c2(96, 64, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    ubos = np.stack([S.make_ubo(cam=(0.1 * i, 0.0, -0.2 * i)) for i in range(4)])
+    out = torch.zeros((4, 64, 96, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    gpu_renderer.set_stream(stream)
+    gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4, timing=True)
+    ms = gpu_renderer.frame_times(4)
+    torch.cuda.synchronize()
+    gpu_renderer.set_stream(None)
+    assert (ms > 0).all()
+    for i in range(4):
+        gpu_renderer.update_ubo(ubos[i])
+        one, _, _ = gpu_renderer.draw_frame(sc.params())
+        assert np.array_equal(out[i].cpu().numpy(), one)

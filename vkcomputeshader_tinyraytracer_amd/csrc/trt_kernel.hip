@@ -22,6 +22,8 @@
 //     (-ffp-contract=off), IEEE-correct division and square root, NaN-ignoring min/max.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../../include/trt/abi.h"
 #include "trt_device.h"
 
@@ -292,27 +294,39 @@ struct Seg {
     int depth;
 };
 
-// LIFO of deferred refraction children.  CAP <= 4: register shift-stack (static indices
-// only, so nothing spills to scratch); larger CAP: private array.
-template <int CAP, bool REG = (CAP <= 4)>
+// LIFO of deferred refraction children.  A workgroup is one wave, so for CAP <= 7 the
+// stack lives in LDS laid out [entry][field][lane]: every push/pop is 8 lane-contiguous
+// ds_write_b32/ds_read_b32 (conflict-free), and no VGPRs hold waiting segments.  Deeper
+// trees (max_depth > 8) use a private array.
+constexpr int LDS_STACK_MAX = 7;
+
+template <int CAP>
+constexpr int lds_stack_floats() { return (CAP >= 1 && CAP <= LDS_STACK_MAX) ? CAP * 8 * 64 : 1; }
+
+template <int CAP, bool LDS = (CAP <= LDS_STACK_MAX)>
 struct DeferStack;
 
 template <int CAP>
 struct DeferStack<CAP, true> {
-    Seg s[CAP > 0 ? CAP : 1];
+    float* base; // this lane's column: base[(e * 8 + f) * 64]
     int n = 0;
+    __device__ __forceinline__ explicit DeferStack(float* lds) : base(lds + threadIdx.x) {}
     __device__ __forceinline__ void push(const Seg& x) {
-#pragma unroll
-        for (int i = (CAP > 0 ? CAP : 1) - 1; i > 0; --i) s[i] = s[i - 1];
-        s[0] = x;
+        float* p = base + n * 8 * 64;
+        p[0] = x.o.x;
+        p[64] = x.o.y;
+        p[128] = x.o.z;
+        p[192] = x.d.x;
+        p[256] = x.d.y;
+        p[320] = x.d.z;
+        p[384] = x.thr;
+        p[448] = __int_as_float(x.depth);
         ++n;
     }
     __device__ __forceinline__ Seg pop() {
-        Seg x = s[0];
-#pragma unroll
-        for (int i = 0; i < (CAP > 0 ? CAP : 1) - 1; ++i) s[i] = s[i + 1];
         --n;
-        return x;
+        const float* p = base + n * 8 * 64;
+        return Seg{mk(p[0], p[64], p[128]), mk(p[192], p[256], p[320]), p[384], __float_as_int(p[448])};
     }
 };
 
@@ -320,15 +334,16 @@ template <int CAP>
 struct DeferStack<CAP, false> {
     Seg s[CAP];
     int n = 0;
+    __device__ __forceinline__ explicit DeferStack(float*) {}
     __device__ __forceinline__ void push(const Seg& x) { s[n++] = x; }
     __device__ __forceinline__ Seg pop() { return s[--n]; }
 };
 
 template <int CAP, bool COUNT>
-__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt) {
+__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt, float* lds) {
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    DeferStack<CAP> stk;
+    DeferStack<CAP> stk(lds);
     Seg cur{orig, dir, 1.0f, 0};
     for (;;) {
         if (COUNT && cur.depth > 0) ++cnt.sec;
@@ -502,36 +517,59 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
     return x;
 }
 
+// One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.
 template <int CAP, bool COUNT>
-__global__ __launch_bounds__(256) void trace_kernel(KArgs A) {
-    // 16x16 pixel tile per workgroup, 8x8 per wave.
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t k = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+__device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
+    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    if (x >= A.width || k >= A.rows) return;
+    const uint32_t y = band_row(A, k);
+    const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
+    const uint32_t spp = A.spp ? A.spp : 1u;
+    f3 acc = mk(0.0f, 0.0f, 0.0f);
+    for (uint32_t s = 0; s < spp; ++s) {
+        f3 d = primary_dir(A, x, y, s);
+        f3 c = cast_ray<CAP, COUNT>(A, orig, d, cnt, lds);
+        acc = (spp == 1u) ? c : add(acc, c);
+    }
+    cnt.pri += spp;
+    if (spp > 1u) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
+    // pow(color, vec3(GAMMA)), shader.comp:598
+    const float gx = powf(acc.x, TRT_GAMMA), gy = powf(acc.y, TRT_GAMMA), gz = powf(acc.z, TRT_GAMMA);
+    const size_t o = (size_t)k * A.width + x;
+    if (A.out32) { // rayOut[idx].resultColor, shader.comp:601
+        reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
+    }
+    if (A.out8) { // rgba8 storage image, shader.comp:61, 600
+        uint32_t r = (uint32_t)floorf(gx * 255.0f + 0.5f);
+        uint32_t g = (uint32_t)floorf(gy * 255.0f + 0.5f);
+        uint32_t b = (uint32_t)floorf(gz * 255.0f + 0.5f);
+        A.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
+    }
+}
+
+// Persistent waves.  The 8x8 tiles are dealt to 8 queues (tile t -> queue t % 8, so every
+// queue gets an even share of the image); a wave drains the queue of its own XCD first
+// (HW_REG_XCC_ID: placement is only a speed hint — one atomic head per XCD instead of one
+// chip-wide head, MI355X_MICROARCH.md "dequeue"), then steals from the others.  The last
+// wave out resets the queue heads, so back-to-back launches on a stream need no memset.
+template <int CAP, bool COUNT>
+__global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
+    __shared__ float lds[lds_stack_floats<CAP>()];
+    const uint32_t lane = threadIdx.x;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     Cnt cnt;
-    if (x < A.width && k < A.rows) {
-        const uint32_t y = band_row(A, k);
-        const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
-        const uint32_t spp = A.spp ? A.spp : 1u;
-        f3 acc = mk(0.0f, 0.0f, 0.0f);
-        for (uint32_t s = 0; s < spp; ++s) {
-            f3 d = primary_dir(A, x, y, s);
-            f3 c = cast_ray<CAP, COUNT>(A, orig, d, cnt);
-            acc = (spp == 1u) ? c : add(acc, c);
-        }
-        cnt.pri = spp;
-        if (spp > 1u) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
-        // pow(color, vec3(GAMMA)), shader.comp:598
-        const float gx = powf(acc.x, TRT_GAMMA), gy = powf(acc.y, TRT_GAMMA), gz = powf(acc.z, TRT_GAMMA);
-        const size_t o = (size_t)k * A.width + x;
-        if (A.out32) { // rayOut[idx].resultColor, shader.comp:601
-            reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
-        }
-        if (A.out8) { // rgba8 storage image, shader.comp:61, 600
-            uint32_t r = (uint32_t)floorf(gx * 255.0f + 0.5f);
-            uint32_t g = (uint32_t)floorf(gy * 255.0f + 0.5f);
-            uint32_t b = (uint32_t)floorf(gz * 255.0f + 0.5f);
-            A.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
+    for (uint32_t s = 0; s < 8u; ++s) {
+        const uint32_t q = (xcc + s) & 7u;
+        for (;;) {
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(&A.sched[q * 16u], 1u);
+            c = __builtin_amdgcn_readfirstlane(c);
+            const uint32_t tile = c * 8u + q;
+            if (tile >= A.ntiles) break;
+            trace_tile<CAP, COUNT>(A, tile, cnt, lds);
         }
     }
     if (COUNT) {
@@ -542,18 +580,37 @@ __global__ __launch_bounds__(256) void trace_kernel(KArgs A) {
             if (lane == 0) atomicAdd(&A.counters[i], w);
         }
     }
+    if (lane == 0) {
+        // Every head fetch of this wave returned before this add (its value was used).
+        const uint32_t d = atomicAdd(&A.sched[8u * 16u], 1u);
+        if (d == gridDim.x - 1u) {
+#pragma unroll
+            for (uint32_t q = 0; q < 8u; ++q) atomicExch(&A.sched[q * 16u], 0u);
+            atomicExch(&A.sched[8u * 16u], 0u);
+        }
+    }
+}
+
+template <typename K>
+static uint32_t resident_waves_per_cu(K kernel) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 64, 0) != hipSuccess || n <= 0) n = 8;
+    return (uint32_t)n;
 }
 
 // Launch helper: picks the deferred-stack capacity from max_depth (children are made only
-// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once).
-hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
-    dim3 block(256);
-    dim3 grid((A.width + 15u) / 16u, (A.rows + 15u) / 16u);
+// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once) and
+// sizes the persistent grid to the resident wave count (never more waves than tiles).
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count, uint32_t num_cus) {
     const uint32_t D = A.max_depth;
-#define TRT_LAUNCH(CAP)                                                              \
-    do {                                                                             \
-        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true>), grid, block, 0, stream, A);  \
-        else hipLaunchKernelGGL((trace_kernel<CAP, false>), grid, block, 0, stream, A);       \
+#define TRT_LAUNCH(CAP)                                                                              \
+    do {                                                                                             \
+        static uint32_t per_cu[2] = {0, 0};                                                          \
+        if (!per_cu[count]) per_cu[count] = count ? resident_waves_per_cu(trace_kernel<CAP, true>)   \
+                                                  : resident_waves_per_cu(trace_kernel<CAP, false>); \
+        const uint32_t nb = std::min<uint32_t>(A.ntiles, num_cus * per_cu[count]);                   \
+        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true>), dim3(nb), dim3(64), 0, stream, A);  \
+        else hipLaunchKernelGGL((trace_kernel<CAP, false>), dim3(nb), dim3(64), 0, stream, A);       \
     } while (0)
     if (D <= 1) TRT_LAUNCH(0);
     else if (D <= 2) TRT_LAUNCH(1);

@@ -20,7 +20,7 @@
 #include "trt_device.h"
 
 namespace trt {
-hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count, uint32_t num_cus);
 }
 
 using trt::BatchRec;
@@ -51,7 +51,11 @@ struct trt_ctx {
     void* d_rays = nullptr;
     size_t caprays = 0;
     unsigned long long* d_counters = nullptr;
+    uint32_t* d_sched = nullptr; // tile-queue heads of the persistent trace kernel
+    uint32_t num_cus = 256;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
+    uint32_t fev_frames = 0;
 };
 
 namespace {
@@ -177,10 +181,15 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipSetDevice(hip_device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&c->d_sched, 256 * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(c->d_sched, 0, 256 * sizeof(uint32_t)) != hipSuccess) {
         trt_destroy(c);
         return TRT_ERR_HIP;
     }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->num_cus = (uint32_t)prop.multiProcessorCount;
     c->stream = c->own_stream;
     *out = c;
     return TRT_OK;
@@ -196,6 +205,8 @@ int trt_destroy(trt_ctx* c) {
     (void)hipFree(c->d_out32);
     (void)hipFree(c->d_rays);
     (void)hipFree(c->d_counters);
+    (void)hipFree(c->d_sched);
+    for (hipEvent_t e : c->fev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -335,8 +346,11 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
     return TRT_OK;
 }
 
-int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt_stats* st) {
-    if (!c) return TRT_ERR_INVALID;
+} // extern "C"
+
+namespace {
+
+int check_params(trt_ctx* c, const trt_params* p) {
     if (!p) return fail(c, TRT_ERR_INVALID, "trt_render: null params");
     if (!c->have_scene) return fail(c, TRT_ERR_NOSCENE, "trt_render: no scene uploaded");
     if (p->width == 0 || p->height == 0 || p->width > 65536 || p->height > 65536)
@@ -348,19 +362,15 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
         return fail(c, TRT_ERR_INVALID, "trt_render: band_index >= band_count");
     if ((p->flags & TRT_FLAG_ENVMAP) && !c->d_env)
         return fail(c, TRT_ERR_INVALID, "trt_render: TRT_FLAG_ENVMAP without an uploaded envmap");
-    HIP_TRY(c, hipSetDevice(c->device));
+    return TRT_OK;
+}
 
-    const bool dev = (p->flags & TRT_FLAG_DEVICE_PTRS) != 0;
-    const bool count = (p->flags & TRT_FLAG_COUNT) != 0 && st;
-    const bool timing = (p->flags & TRT_FLAG_TIMING) != 0 && st;
-    const uint32_t rows = trt_output_rows(p);
-    const size_t npx = (size_t)rows * p->width;
-
-    KArgs A;
+// Everything of KArgs that does not depend on the UBO or the output pointers.
+void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     std::memset(&A, 0, sizeof(A));
     A.width = p->width;
     A.height = p->height;
-    A.rows = rows;
+    A.rows = trt_output_rows(p);
     A.band_rows = p->band_rows;
     A.band_count = p->band_count;
     A.band_index = p->band_index;
@@ -380,8 +390,77 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     A.env_w = c->env_w;
     A.env_h = c->env_h;
     A.counters = c->d_counters;
+    A.sched = c->d_sched;
+    A.ntx = (A.width + 7u) / 8u;
+    A.ntiles = A.ntx * ((A.rows + 7u) / 8u);
+}
 
-    int rc;
+} // namespace
+
+extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
+                                 uint8_t* out8, size_t frame_stride) {
+    if (!c) return TRT_ERR_INVALID;
+    int rc = check_params(c, p);
+    if (rc != TRT_OK) return rc;
+    if (!(p->flags & TRT_FLAG_DEVICE_PTRS))
+        return fail(c, TRT_ERR_INVALID, "trt_render_frames: needs TRT_FLAG_DEVICE_PTRS");
+    if (p->flags & TRT_FLAG_COUNT)
+        return fail(c, TRT_ERR_INVALID, "trt_render_frames: COUNT is a per-frame trt_render flag");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const bool timing = (p->flags & TRT_FLAG_TIMING) != 0;
+    if (timing) {
+        while (c->fev.size() < 2 * (size_t)nframes) {
+            hipEvent_t e;
+            HIP_TRY(c, hipEventCreate(&e));
+            c->fev.push_back(e);
+        }
+        c->fev_frames = nframes;
+    }
+    KArgs A;
+    fill_args(c, p, A);
+    A.rays_in = reinterpret_cast<const float*>(p->rays_in);
+    if (A.rows == 0) return TRT_OK;
+    for (uint32_t i = 0; i < nframes; ++i) {
+        if (ubos) {
+            c->ubo = ubos[i];
+            fill_ubo_args(A, c->ubo);
+        }
+        A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
+        if (timing) HIP_TRY(c, hipEventRecord(c->fev[2 * i], c->stream));
+        HIP_TRY(c, trt::launch_trace(A, c->stream, false, c->num_cus));
+        if (timing) HIP_TRY(c, hipEventRecord(c->fev[2 * i + 1], c->stream));
+    }
+    return TRT_OK;
+}
+
+extern "C" int trt_frame_times(trt_ctx* c, float* ms, uint32_t n) {
+    if (!c || (!ms && n)) return TRT_ERR_INVALID;
+    if (n > c->fev_frames) return fail(c, TRT_ERR_INVALID, "trt_frame_times: more frames than were timed");
+    HIP_TRY(c, hipSetDevice(c->device));
+    for (uint32_t i = 0; i < n; ++i) {
+        HIP_TRY(c, hipEventSynchronize(c->fev[2 * i + 1]));
+        HIP_TRY(c, hipEventElapsedTime(&ms[i], c->fev[2 * i], c->fev[2 * i + 1]));
+    }
+    return TRT_OK;
+}
+
+extern "C" {
+
+int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt_stats* st) {
+    if (!c) return TRT_ERR_INVALID;
+    int rc = check_params(c, p);
+    if (rc != TRT_OK) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+
+    const bool dev = (p->flags & TRT_FLAG_DEVICE_PTRS) != 0;
+    const bool count = (p->flags & TRT_FLAG_COUNT) != 0 && st;
+    const bool timing = (p->flags & TRT_FLAG_TIMING) != 0 && st;
+    const uint32_t rows = trt_output_rows(p);
+    const size_t npx = (size_t)rows * p->width;
+
+    KArgs A;
+    fill_args(c, p, A);
+
     if (p->rays_in) {
         if (dev) {
             A.rays_in = reinterpret_cast<const float*>(p->rays_in);
@@ -410,7 +489,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     }
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-    if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
+    if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count, c->num_cus));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
     if (out8 && !dev)
         HIP_TRY(c, hipMemcpyAsync(out8, c->d_out8, npx * 4, hipMemcpyDeviceToHost, c->stream));

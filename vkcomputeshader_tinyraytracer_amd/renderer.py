@@ -56,9 +56,15 @@ class Renderer:
         self._check(self._L.trt_update_ubo(self._h, u.ctypes.data))
 
     def set_stream(self, stream) -> None:
-        """`stream`: a torch.cuda.Stream, a raw hipStream_t int, or None (own stream)."""
+        """`stream`: a torch.cuda.Stream (not the legacy default stream), a raw hipStream_t
+        int, or None (the context's own stream)."""
+        if stream is None:
+            self._check(self._L.trt_set_stream(self._h, None))
+            return
         s = getattr(stream, "cuda_stream", stream)
-        self._check(self._L.trt_set_stream(self._h, ctypes.c_void_p(s) if s else None))
+        if not s:
+            raise ValueError("the legacy null stream cannot be selected; use a torch.cuda.Stream()")
+        self._check(self._L.trt_set_stream(self._h, ctypes.c_void_p(s)))
 
     def synchronize(self) -> None:
         self._check(self._L.trt_synchronize(self._h))
@@ -107,6 +113,34 @@ class Renderer:
         st = T.Stats()
         self._check(self._L.trt_render(self._h, ctypes.byref(p), o8, o32, ctypes.byref(st)))
         return out8, out32, st.as_dict()
+
+    def render_frames(self, params: T.Params, out8, nframes: int, ubos: np.ndarray | None = None,
+                      frame_stride: int = 0, timing: bool = False) -> None:
+        """Native frame loop (trt_render_frames): `nframes` launches enqueued back to back on
+        the context's stream into the device tensor `out8` (+ i * frame_stride bytes)."""
+        if not _is_torch_cuda(out8):
+            raise ValueError("render_frames renders into a device (torch CUDA) tensor")
+        p = T.Params.from_buffer_copy(params)
+        p.flags |= T.FLAG_DEVICE_PTRS
+        p.flags &= ~T.FLAG_COUNT
+        if timing:
+            p.flags |= T.FLAG_TIMING
+        else:
+            p.flags &= ~T.FLAG_TIMING
+        rows = int(self._L.trt_output_rows(ctypes.byref(p)))
+        need = rows * p.width * 4 + (nframes - 1) * frame_stride
+        assert out8.is_contiguous() and out8.numel() >= need
+        u = None
+        if ubos is not None:
+            u = np.ascontiguousarray(ubos, T.UBO)
+            assert u.shape[0] >= nframes
+        self._check(self._L.trt_render_frames(self._h, ctypes.byref(p), u.ctypes.data if u is not None else None,
+                                              nframes, out8.data_ptr(), frame_stride))
+
+    def frame_times(self, n: int) -> np.ndarray:
+        ms = (ctypes.c_float * n)()
+        self._check(self._L.trt_frame_times(self._h, ms, n))
+        return np.frombuffer(ms, np.float32).copy()
 
     def close(self) -> None:
         if getattr(self, "_h", None):
