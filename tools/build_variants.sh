@@ -1,0 +1,37 @@
+#!/usr/bin/env bash
+# Experimental builds of libtrt.so for A/B timing (loaded with TRT_LIB=diag/libtrt_<name>.so).
+# Diagnostic variants change results (they price one stage) and are never the product.
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SRC=$ROOT/vkcomputeshader_tinyraytracer_amd/csrc
+OUT=$ROOT/diag
+mkdir -p "$OUT" "$ROOT/build/diag"
+FP="-ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math -fno-slp-vectorize"
+HOST="-O2 -std=c++17 -fPIC -ffp-contract=off -I/opt/rocm/include -D__HIP_PLATFORM_AMD__"
+for f in trt_runtime scene_build obj_load; do
+    [ "$ROOT/build/diag/$f.o" -nt "$SRC/$f.cpp" ] || /opt/rocm/bin/hipcc $HOST -x c++ -c -o "$ROOT/build/diag/$f.o" "$SRC/$f.cpp"
+done
+variant() { # name extra-flags...
+    local name=$1
+    shift
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "$@" -c -o "$ROOT/build/diag/k_$name.o" "$SRC/trt_kernel.hip"
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libtrt_$name.so" "$ROOT/build/diag/k_$name.o" \
+        "$ROOT/build/diag/trt_runtime.o" "$ROOT/build/diag/scene_build.o" "$ROOT/build/diag/obj_load.o"
+    echo "built $OUT/libtrt_$name.so"
+}
+for v in "$@"; do
+    case $v in
+        base) variant base ;;
+        nslp) variant nslp -fno-slp-vectorize ;;
+        noshadow) variant noshadow -DTRT_DIAG_NO_SHADOW ;;
+        nopow) variant nopow -DTRT_DIAG_NO_POW ;;
+        fastdiv) variant fastdiv -fno-hip-fp32-correctly-rounded-divide-sqrt ;;
+        tpw2) variant tpw2 -DTRT_TPW=2 ;;
+        npow) variant npow -DTRT_NATIVE_POW ;;
+        trivial) variant trivial -DTRT_DIAG_TRIVIAL -DTRT_NATIVE_POW -fno-slp-vectorize ;;
+        npow_nslp) variant npow_nslp -DTRT_NATIVE_POW -fno-slp-vectorize ;;
+        npow_nslp_fdiv) variant npow_nslp_fdiv -DTRT_NATIVE_POW -fno-slp-vectorize -fno-hip-fp32-correctly-rounded-divide-sqrt ;;
+        tpw4) variant tpw4 -DTRT_TPW=4 ;;
+        *) echo "unknown variant $v"; exit 2 ;;
+    esac
+done

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Quick kernel-time probe: median / min per-frame device time of the trace kernel for one
+configuration (HIP events around each launch), no CPU baseline.
+
+  python tools/kbench.py [--config C2] [--frames 100] [--width W --height H] [--depth D]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--frames", type=int, default=100)
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--depth", type=int, default=0)
+    ap.add_argument("--tag", default="")
+    ap.add_argument("--flags", type=lambda v: int(v, 0), default=None, help="override trt_params.flags")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+    from vkcomputeshader_tinyraytracer_amd import scene as S
+
+    kw = {}
+    if a.width:
+        kw = dict(width=a.width, height=a.height)
+    if a.config == "ref":
+        sc = S.config_reference_default(**kw)
+    else:
+        sc = S.CONFIGS[a.config](**kw)
+    if a.depth:
+        sc.max_depth = a.depth
+    if a.flags is not None:
+        sc.flags = a.flags
+    p = sc.params()
+    r = trt.Renderer(0)
+    r.upload_scene(sc)
+    _, _, st = r.draw_frame(p, count=True)
+    out = torch.empty((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    r.set_stream(stream)
+    r.render_frames(p, out, 5)
+    r.render_frames(p, out, a.frames, timing=True)
+    ms = r.frame_times(a.frames)
+    torch.cuda.synchronize()
+    rays = st["primary_rays"] + st["secondary_rays"]
+    res = {"tag": a.tag, "sched": os.environ.get("TRT_SCHED", "persistent"), "config": a.config,
+           "size": [p.width, p.height], "depth": p.max_depth, "rays": rays,
+           "med_us": round(float(np.median(ms)) * 1e3, 2), "min_us": round(float(ms.min()) * 1e3, 2),
+           "Mray_s_kernel": round(rays / (float(np.median(ms)) * 1e-3) / 1e6, 1)}
+    print(json.dumps(res), flush=True)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -13,7 +13,8 @@ from pathlib import Path
 from .types import Params, Stats
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libtrt.so"
+# TRT_LIB may point at an experimental build of the same library (tools/build_variants.sh).
+LIB_PATH = Path(os.environ["TRT_LIB"]) if os.environ.get("TRT_LIB") else _HERE / "libtrt.so"
 
 _lib: ctypes.CDLL | None = None
 

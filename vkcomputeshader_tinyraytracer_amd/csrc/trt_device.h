@@ -79,7 +79,6 @@ struct KArgs {
     uint32_t* __restrict__ out8;       // packed RGBA8, or null
     float* __restrict__ out32;         // float4 per pixel, or null
     unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
-    uint32_t* __restrict__ sched; // 8 tile-queue heads (64 B apart) + done count; zero between launches
     uint32_t ntx;                 // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
 };

@@ -22,7 +22,6 @@
 //     (-ffp-contract=off), IEEE-correct division and square root, NaN-ignoring min/max.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 
 #include "../../include/trt/abi.h"
 #include "trt_device.h"
@@ -57,6 +56,19 @@ __device__ __forceinline__ f3 reflect3(f3 I, f3 N) {
     return sub(I, muls(N, k));
 }
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+// pow(x, y) for x >= 0, y > 0 (the only uses: the Phong exponent, shader.comp:502, and
+// gamma, :598) as exp2(y * log2(x)) on the transcendental units (v_log_f32 / v_exp_f32):
+// the form GLSL pow takes on GPUs (the Vulkan spec allows 3 + 2|x*log2 y| ulp).  x = 0 ->
+// log2 = -inf -> exp2(-inf) = 0.  ocml's correctly-rounded-ish powf cost 14 us of a 61 us C2
+// frame; the difference to the oracle's libm powf is a few ulp (tests/helpers.py FLOAT_TOL).
+#ifdef TRT_LIBM_POW
+__device__ __forceinline__ float pow_pos(float x, float y) { return powf(x, y); }
+#else
+__device__ __forceinline__ float pow_pos(float x, float y) {
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
+#endif
 __device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
 // ---- primitives (shader.comp line refs) -------------------------------------------------
@@ -194,6 +206,9 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
 // shadow_intersect, shader.comp:364-399: any hit on spheres / triangles; floor excluded.
 template <bool COUNT>
 __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, float max_dist, Cnt& c) {
+#ifdef TRT_DIAG_NO_SHADOW
+    return false; // diagnostic build only: prices the shadow rays
+#endif
     if (A.flags & TRT_FLAG_SPHERES) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -416,7 +431,11 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
                 float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
                 diffuse = add(diffuse, muls(kdv, diff));
                 f3 rdir = reflect3(neg(ld), n);
-                float spec = 1.0f * powf(fmaxf(0.0f, dot3(rdir, v)), sexp);
+#ifdef TRT_DIAG_NO_POW
+                float spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
+#else
+                float spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
+#endif
                 specular = add(specular, muls(kdv, spec));
             }
             color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
@@ -524,6 +543,10 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;
+#ifdef TRT_DIAG_TRIVIAL
+    if (A.out8) A.out8[(size_t)k * A.width + x] = 0xff000000u | x; // diagnostic: launch + store only
+    return;
+#endif
     const uint32_t y = band_row(A, k);
     const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
     const uint32_t spp = A.spp ? A.spp : 1u;
@@ -536,7 +559,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     cnt.pri += spp;
     if (spp > 1u) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
     // pow(color, vec3(GAMMA)), shader.comp:598
-    const float gx = powf(acc.x, TRT_GAMMA), gy = powf(acc.y, TRT_GAMMA), gz = powf(acc.z, TRT_GAMMA);
+    const float gx = pow_pos(acc.x, TRT_GAMMA), gy = pow_pos(acc.y, TRT_GAMMA), gz = pow_pos(acc.z, TRT_GAMMA);
     const size_t o = (size_t)k * A.width + x;
     if (A.out32) { // rayOut[idx].resultColor, shader.comp:601
         reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
@@ -549,68 +572,44 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     }
 }
 
-// Persistent waves.  The 8x8 tiles are dealt to 8 queues (tile t -> queue t % 8, so every
-// queue gets an even share of the image); a wave drains the queue of its own XCD first
-// (HW_REG_XCC_ID: placement is only a speed hint — one atomic head per XCD instead of one
-// chip-wide head, MI355X_MICROARCH.md "dequeue"), then steals from the others.  The last
-// wave out resets the queue heads, so back-to-back launches on a stream need no memset.
+// One 64-lane workgroup per 8x8 tile.  The hardware dispatcher hands each freed wave slot
+// the next tile, which balances the very uneven per-tile cost (sky vs. glass sphere) with
+// no atomics.  (Measured on C2: a persistent grid pulling tiles from per-XCD atomic queue
+// heads was 1.5-4.5x slower — 12,288 dequeues per ~60 us frame saturate the heads — and a
+// static grid-stride over the resident waves 1.2-2x slower from imbalance.)
 template <int CAP, bool COUNT>
 __global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
-    const uint32_t lane = threadIdx.x;
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     Cnt cnt;
-    for (uint32_t s = 0; s < 8u; ++s) {
-        const uint32_t q = (xcc + s) & 7u;
-        for (;;) {
-            uint32_t c = 0;
-            if (lane == 0) c = atomicAdd(&A.sched[q * 16u], 1u);
-            c = __builtin_amdgcn_readfirstlane(c);
-            const uint32_t tile = c * 8u + q;
-            if (tile >= A.ntiles) break;
-            trace_tile<CAP, COUNT>(A, tile, cnt, lds);
-        }
-    }
+#ifdef TRT_TPW
+    for (uint32_t t = blockIdx.x * TRT_TPW; t < min(A.ntiles, (blockIdx.x + 1) * TRT_TPW); ++t)
+        trace_tile<CAP, COUNT>(A, t, cnt, lds);
+#else
+    trace_tile<CAP, COUNT>(A, blockIdx.x, cnt, lds);
+#endif
     if (COUNT) {
         const uint32_t v[9] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt};
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             unsigned long long w = wave_sum((unsigned long long)v[i]);
-            if (lane == 0) atomicAdd(&A.counters[i], w);
+            if (threadIdx.x == 0) atomicAdd(&A.counters[i], w);
         }
     }
-    if (lane == 0) {
-        // Every head fetch of this wave returned before this add (its value was used).
-        const uint32_t d = atomicAdd(&A.sched[8u * 16u], 1u);
-        if (d == gridDim.x - 1u) {
-#pragma unroll
-            for (uint32_t q = 0; q < 8u; ++q) atomicExch(&A.sched[q * 16u], 0u);
-            atomicExch(&A.sched[8u * 16u], 0u);
-        }
-    }
-}
-
-template <typename K>
-static uint32_t resident_waves_per_cu(K kernel) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 64, 0) != hipSuccess || n <= 0) n = 8;
-    return (uint32_t)n;
 }
 
 // Launch helper: picks the deferred-stack capacity from max_depth (children are made only
-// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once) and
-// sizes the persistent grid to the resident wave count (never more waves than tiles).
-hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count, uint32_t num_cus) {
+// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once).
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const uint32_t D = A.max_depth;
-#define TRT_LAUNCH(CAP)                                                                              \
-    do {                                                                                             \
-        static uint32_t per_cu[2] = {0, 0};                                                          \
-        if (!per_cu[count]) per_cu[count] = count ? resident_waves_per_cu(trace_kernel<CAP, true>)   \
-                                                  : resident_waves_per_cu(trace_kernel<CAP, false>); \
-        const uint32_t nb = std::min<uint32_t>(A.ntiles, num_cus * per_cu[count]);                   \
-        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true>), dim3(nb), dim3(64), 0, stream, A);  \
-        else hipLaunchKernelGGL((trace_kernel<CAP, false>), dim3(nb), dim3(64), 0, stream, A);       \
+#ifdef TRT_TPW
+    const dim3 grid((A.ntiles + TRT_TPW - 1) / TRT_TPW), block(64);
+#else
+    const dim3 grid(A.ntiles), block(64);
+#endif
+#define TRT_LAUNCH(CAP)                                                                      \
+    do {                                                                                     \
+        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true>), grid, block, 0, stream, A); \
+        else hipLaunchKernelGGL((trace_kernel<CAP, false>), grid, block, 0, stream, A);      \
     } while (0)
     if (D <= 1) TRT_LAUNCH(0);
     else if (D <= 2) TRT_LAUNCH(1);

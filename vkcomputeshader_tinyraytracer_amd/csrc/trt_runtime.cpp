@@ -20,7 +20,7 @@
 #include "trt_device.h"
 
 namespace trt {
-hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count, uint32_t num_cus);
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
 }
 
 using trt::BatchRec;
@@ -51,7 +51,6 @@ struct trt_ctx {
     void* d_rays = nullptr;
     size_t caprays = 0;
     unsigned long long* d_counters = nullptr;
-    uint32_t* d_sched = nullptr; // tile-queue heads of the persistent trace kernel
     uint32_t num_cus = 256;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
@@ -181,9 +180,7 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipSetDevice(hip_device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&c->d_sched, 256 * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(c->d_sched, 0, 256 * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess) {
         trt_destroy(c);
         return TRT_ERR_HIP;
     }
@@ -205,7 +202,6 @@ int trt_destroy(trt_ctx* c) {
     (void)hipFree(c->d_out32);
     (void)hipFree(c->d_rays);
     (void)hipFree(c->d_counters);
-    (void)hipFree(c->d_sched);
     for (hipEvent_t e : c->fev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -390,7 +386,6 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.env_w = c->env_w;
     A.env_h = c->env_h;
     A.counters = c->d_counters;
-    A.sched = c->d_sched;
     A.ntx = (A.width + 7u) / 8u;
     A.ntiles = A.ntx * ((A.rows + 7u) / 8u);
 }
@@ -427,7 +422,7 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
         }
         A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
         if (timing) HIP_TRY(c, hipEventRecord(c->fev[2 * i], c->stream));
-        HIP_TRY(c, trt::launch_trace(A, c->stream, false, c->num_cus));
+        HIP_TRY(c, trt::launch_trace(A, c->stream, false));
         if (timing) HIP_TRY(c, hipEventRecord(c->fev[2 * i + 1], c->stream));
     }
     return TRT_OK;
@@ -489,7 +484,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     }
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-    if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count, c->num_cus));
+    if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
     if (out8 && !dev)
         HIP_TRY(c, hipMemcpyAsync(out8, c->d_out8, npx * 4, hipMemcpyDeviceToHost, c->stream));
