@@ -84,6 +84,9 @@ typedef struct trt_stats {
     uint64_t batch_tests;    /* ray_aabb_intersect calls (scene + shadow) */
     uint64_t batch_hits;     /* ... that passed */
     uint64_t tri_tests;      /* ray_triangle_intersect calls (scene + shadow) */
+    uint64_t node_tests;     /* hierarchy-node box tests in front of the batch tests (0 in the
+                                reference's linear loop; batch_tests then counts only the batch
+                                boxes actually reached) */
     double kernel_ms;        /* device time of the frame (TRT_FLAG_TIMING) */
 } trt_stats;
 

@@ -752,6 +752,7 @@ int orc_render(const orc_scene* sc, const trt_params* p, int mode, int nthreads,
                             &st->tri_nearest, &st->sphere_tests, &st->batch_tests, &st->batch_hits,
                             &st->tri_tests};
         for (int i = 0; i < 9; ++i) *dst[i] = atomic_load(&J.acc[i]);
+        st->node_tests = 0; /* the reference walks its batch list linearly */
         st->kernel_ms = 0.0;
     }
     return TRT_OK;
@@ -831,6 +832,7 @@ void orc_cast_ray(const orc_scene* sc, const trt_params* p, int mode, const floa
         st->batch_tests = cnt.batch_tests;
         st->batch_hits = cnt.batch_hits;
         st->tri_tests = cnt.tri_tests;
+        st->node_tests = 0; /* the reference walks its batch list linearly */
         st->kernel_ms = 0.0;
     }
 }

@@ -16,7 +16,7 @@ SMALL_ENV = (1024, 512)
 
 
 def _counts(st):
-    return tuple(st[k] for k in T.Stats.COUNTERS)
+    return tuple(st[k] for k in T.Stats.EXACT)
 
 
 def _check(r, sc, params=None, want32=True, max_frac=0.02):

@@ -22,16 +22,12 @@ variant() { # name extra-flags...
 for v in "$@"; do
     case $v in
         base) variant base ;;
-        nslp) variant nslp -fno-slp-vectorize ;;
         noshadow) variant noshadow -DTRT_DIAG_NO_SHADOW ;;
         nopow) variant nopow -DTRT_DIAG_NO_POW ;;
         fastdiv) variant fastdiv -fno-hip-fp32-correctly-rounded-divide-sqrt ;;
-        tpw2) variant tpw2 -DTRT_TPW=2 ;;
-        npow) variant npow -DTRT_NATIVE_POW ;;
-        trivial) variant trivial -DTRT_DIAG_TRIVIAL -DTRT_NATIVE_POW -fno-slp-vectorize ;;
-        npow_nslp) variant npow_nslp -DTRT_NATIVE_POW -fno-slp-vectorize ;;
-        npow_nslp_fdiv) variant npow_nslp_fdiv -DTRT_NATIVE_POW -fno-slp-vectorize -fno-hip-fp32-correctly-rounded-divide-sqrt ;;
-        tpw4) variant tpw4 -DTRT_TPW=4 ;;
+        xcd) variant xcd -DTRT_XCD_SWIZZLE ;;
+        libmpow) variant libmpow -DTRT_LIBM_POW ;;
+        trivial) variant trivial -DTRT_DIAG_TRIVIAL ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac
 done

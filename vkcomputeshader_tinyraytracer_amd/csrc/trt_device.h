@@ -11,6 +11,8 @@
 
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
 namespace trt {
 
 // One AABB batch (Model, shader.comp:29-38): bbox + triangle range + smooth flag.
@@ -79,7 +81,10 @@ struct KArgs {
     uint32_t* __restrict__ out8;       // packed RGBA8, or null
     float* __restrict__ out32;         // float4 per pixel, or null
     unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
-    uint32_t ntx;                 // 8x8 tiles per output row
+    const float4* __restrict__ nodes; // batch hierarchy: per node (lo.xyz, -), (hi.xyz, -)
+    uint32_t node_off[11];            // first node of level L (L = 1..top) in `nodes`
+    uint32_t top;                     // levels above the batches: 8^top >= nbatch
+    uint32_t ntx;                     // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
 };
 

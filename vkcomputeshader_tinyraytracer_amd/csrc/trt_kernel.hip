@@ -116,7 +116,7 @@ enum : int { HIT_NONE = 0, HIT_FLOOR = 1, HIT_SPHERE = 2, HIT_TRI = 3 };
 
 // Per-lane work counters (COUNT builds only): the units of trt_stats.
 struct Cnt {
-    uint32_t pri = 0, sec = 0, sh = 0, miss = 0, trin = 0, sph = 0, bt = 0, bh = 0, tt = 0;
+    uint32_t pri = 0, sec = 0, sh = 0, miss = 0, trin = 0, sph = 0, bt = 0, bh = 0, tt = 0, nt = 0;
 };
 
 struct Hit {
@@ -127,8 +127,130 @@ struct Hit {
     int ni; // normal interpolation flag of the batch that produced the triangle hit
 };
 
-template <bool COUNT>
-__device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit& h, Cnt& c) {
+// ---- batch walk: implicit 8-ary range hierarchy + the reference batch test -----------------
+//
+// Level 0 is the reference's batch list (Model records, shader.comp:338); level L >= 1 node k
+// is the exact union box of batches [k*8^L, (k+1)*8^L).  The wave walks the tree depth-first,
+// left to right, so leaves are visited in increasing batch index — the reference's loop
+// order, which keeps its first-index-wins tie-break (strict `<`, shader.comp:349).  A lane
+// that misses a node skips the node's whole range (`skip`); a lane reaching a leaf runs the
+// reference's exact ray_aabb_intersect.  Internal nodes use node_hit(), which treats a slab
+// whose product is NaN (0*inf: origin on the plane, zero direction component) as
+// unconstrained; with that rule a node miss implies a miss of every batch below it
+// (monotone FP32 rounding; tests/test_hierarchy_conservative.py), so the set of batches a
+// lane tests triangles in is exactly the reference's.
+__device__ __forceinline__ bool node_hit(f3 o, f3 inv, const float4& lo, const float4& hi) {
+    const float INF = __builtin_huge_valf();
+    float t0x = (lo.x - o.x) * inv.x, t1x = (hi.x - o.x) * inv.x;
+    float t0y = (lo.y - o.y) * inv.y, t1y = (hi.y - o.y) * inv.y;
+    float t0z = (lo.z - o.z) * inv.z, t1z = (hi.z - o.z) * inv.z;
+    const bool nx = (t0x != t0x) || (t1x != t1x);
+    const bool ny = (t0y != t0y) || (t1y != t1y);
+    const bool nz = (t0z != t0z) || (t1z != t1z);
+    const float mnx = nx ? -INF : fminf(t0x, t1x), mxx = nx ? INF : fmaxf(t0x, t1x);
+    const float mny = ny ? -INF : fminf(t0y, t1y), mxy = ny ? INF : fmaxf(t0y, t1y);
+    const float mnz = nz ? -INF : fminf(t0z, t1z), mxz = nz ? INF : fmaxf(t0z, t1z);
+    const float tNear = fmaxf(fmaxf(mnx, mny), mnz);
+    const float tFar = fminf(fminf(mxx, mxy), mxz);
+    return tNear <= tFar && tFar > TRT_EPS;
+}
+
+// SHADOW = false: closest hit into h (shader.comp:338-361).  SHADOW = true: any hit with
+// MIN_EPSILON < t < max_dist sets `occluded` (shader.comp:379-396).  A hit batch's triangles
+// (v0, e1, e2: 48 B each) are staged through LDS 64 at a time by one coalesced load per
+// lane, then read back as wave-wide broadcasts.
+template <bool COUNT, bool SHADOW>
+__device__ __forceinline__ void walk_batches(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
+                                             float max_dist, Cnt& c, float4* slab) {
+    const uint32_t nb = A.nbatch, top = A.top;
+    uint32_t s = 0, L = top, skip = 0;
+    while (s < nb) {
+        const bool part = (!SHADOW || !occluded) && s >= skip;
+        bool hit;
+        BatchRec rec;
+        if (L == 0) {
+            rec = A.batches[s]; // wave-uniform: scalar load
+            hit = part && aabb_hit(o, inv, rec.bmin, rec.bmax);
+            if (COUNT && part) {
+                ++c.bt;
+                c.bh += hit ? 1u : 0u;
+            }
+        } else {
+            const float4* nd = A.nodes + 2u * (A.node_off[L] + (s >> (3u * L)));
+            const float4 lo = nd[0], hi = nd[1];
+            hit = part && node_hit(o, inv, lo, hi);
+            if (COUNT && part) ++c.nt;
+        }
+        const uint32_t span = 1u << (3u * L);
+        if (part && !hit) skip = s + span;
+        if (__ballot(hit) == 0) {
+            if (SHADOW && __ballot(!occluded) == 0) return;
+            s += span;
+        } else if (L > 0) {
+            --L; // descend into the first child; same start
+            continue;
+        } else {
+            const int start = rec.start;
+            const int count = rec.count_ni & 0x7fffffff;
+            const int ni = (rec.count_ni >> 31) & 1;
+            // The lanes still active here (not every lane of the tile: edge pixels and lanes
+            // whose ray tree is done are masked) stage the slab together, by active-lane rank.
+            const uint64_t act = __ballot(true);
+            const uint32_t nact = (uint32_t)__popcll(act);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+            for (int base = 0; base < count; base += 64) {
+                const int n = min(64, count - base);
+                __syncthreads(); // one wave per workgroup: orders the LDS reads of the previous slab
+                for (uint32_t i = rank; i < (uint32_t)n; i += nact) {
+                    const float4* g = reinterpret_cast<const float4*>(A.geo + start + base + (int)i);
+                    slab[i * 3u + 0u] = g[0];
+                    slab[i * 3u + 1u] = g[1];
+                    slab[i * 3u + 2u] = g[2];
+                }
+                __syncthreads();
+                if (hit) {
+                    for (int k = 0; k < n; ++k) { // shader.comp:344-359 / 384-393
+                        const float4 ga = slab[k * 3 + 0], gb = slab[k * 3 + 1], gc = slab[k * 3 + 2];
+                        if (COUNT) ++c.tt;
+                        const f3 v0 = mk(ga.x, ga.y, ga.z), e1 = mk(ga.w, gb.x, gb.y), e2 = mk(gb.z, gb.w, gc.x);
+                        f3 hv = cross3(d, e2);
+                        float a = dot3(e1, hv);
+                        if (a > -TRT_EPS && a < TRT_EPS) continue;
+                        float f = 1.0f / a;
+                        f3 sv = sub(o, v0);
+                        float u = f * dot3(sv, hv);
+                        if (u < 0.0f || u > 1.0f) continue;
+                        f3 q = cross3(sv, e1);
+                        float v = f * dot3(d, q);
+                        if (v < 0.0f || u + v > 1.0f) continue;
+                        float t = f * dot3(e2, q);
+                        if (t <= TRT_EPS) continue;
+                        if (SHADOW) {
+                            if (t > TRT_EPS && t < max_dist) {
+                                occluded = true;
+                                break;
+                            }
+                        } else if (t > TRT_EPS && t < h.t) {
+                            h.t = t;
+                            h.kind = HIT_TRI;
+                            h.idx = start + base + k;
+                            h.u = u;
+                            h.v = v;
+                            h.ni = ni;
+                        }
+                    }
+                }
+            }
+            if (SHADOW && __ballot(!occluded) == 0) return;
+            s += 1;
+        }
+        while (L < top && (s & ((1u << (3u * (L + 1u))) - 1u)) == 0u) ++L; // climb to the aligned level
+    }
+}
+
+template <bool COUNT, bool MESH>
+__device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit& h, Cnt& c, float4* slab) {
     h.t = 1e10f;
     h.kind = HIT_NONE;
     h.idx = 0;
@@ -159,53 +281,16 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
             }
         }
     }
-    const uint32_t nb = A.nbatch;
-    if (nb == 0) return;
+    if (!MESH || A.nbatch == 0) return;
     f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:336
-    for (uint32_t b = 0; b < nb; ++b) {              // shader.comp:338
-        const BatchRec rec = A.batches[b];           // wave-uniform: scalar load
-        bool hitbox = aabb_hit(o, inv, rec.bmin, rec.bmax);
-        if (COUNT) {
-            ++c.bt;
-            c.bh += hitbox ? 1u : 0u;
-        }
-        if (__ballot(hitbox) == 0) continue; // no lane of the wave enters this batch
-        if (hitbox) {
-            const int start = rec.start;
-            const int count = rec.count_ni & 0x7fffffff;
-            const int ni = (rec.count_ni >> 31) & 1;
-            for (int j = start; j < start + count; ++j) { // shader.comp:344-359
-                const TriGeo g = A.geo[j];                  // wave-uniform: scalar loads
-                if (COUNT) ++c.tt;
-                f3 e1 = ld3(g.e1), e2 = ld3(g.e2), v0 = ld3(g.v0);
-                f3 hv = cross3(d, e2);
-                float a = dot3(e1, hv);
-                if (a > -TRT_EPS && a < TRT_EPS) continue;
-                float f = 1.0f / a;
-                f3 s = sub(o, v0);
-                float u = f * dot3(s, hv);
-                if (u < 0.0f || u > 1.0f) continue;
-                f3 q = cross3(s, e1);
-                float v = f * dot3(d, q);
-                if (v < 0.0f || u + v > 1.0f) continue;
-                float t = f * dot3(e2, q);
-                if (t <= TRT_EPS) continue;
-                if (t > TRT_EPS && t < h.t) {
-                    h.t = t;
-                    h.kind = HIT_TRI;
-                    h.idx = j;
-                    h.u = u;
-                    h.v = v;
-                    h.ni = ni;
-                }
-            }
-        }
-    }
+    bool unused = false;
+    walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
 }
 
 // shadow_intersect, shader.comp:364-399: any hit on spheres / triangles; floor excluded.
-template <bool COUNT>
-__device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, float max_dist, Cnt& c) {
+template <bool COUNT, bool MESH>
+__device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, float max_dist, Cnt& c,
+                                                 float4* slab) {
 #ifdef TRT_DIAG_NO_SHADOW
     return false; // diagnostic build only: prices the shadow rays
 #endif
@@ -217,47 +302,11 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
             if (sphere_hit(o, d, A.sph[i], t) && t < max_dist) return true;
         }
     }
-    const uint32_t nb = A.nbatch;
-    if (nb == 0) return false;
-    f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if (!MESH || A.nbatch == 0) return false;
+    f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:377
     bool occluded = false;
-    for (uint32_t b = 0; b < nb; ++b) {
-        const BatchRec rec = A.batches[b];
-        bool hitbox = !occluded && aabb_hit(o, inv, rec.bmin, rec.bmax);
-        if (COUNT && !occluded) {
-            ++c.bt;
-            c.bh += hitbox ? 1u : 0u;
-        }
-        if (__ballot(hitbox) == 0) {
-            if (__ballot(!occluded) == 0) break;
-            continue;
-        }
-        if (hitbox) {
-            const int start = rec.start;
-            const int count = rec.count_ni & 0x7fffffff;
-            for (int j = start; j < start + count; ++j) {
-                const TriGeo g = A.geo[j];
-                if (COUNT) ++c.tt;
-                f3 e1 = ld3(g.e1), e2 = ld3(g.e2), v0 = ld3(g.v0);
-                f3 hv = cross3(d, e2);
-                float a = dot3(e1, hv);
-                if (a > -TRT_EPS && a < TRT_EPS) continue;
-                float f = 1.0f / a;
-                f3 s = sub(o, v0);
-                float u = f * dot3(s, hv);
-                if (u < 0.0f || u > 1.0f) continue;
-                f3 q = cross3(s, e1);
-                float v = f * dot3(d, q);
-                if (v < 0.0f || u + v > 1.0f) continue;
-                float t = f * dot3(e2, q);
-                if (t <= TRT_EPS) continue;
-                if (t > TRT_EPS && t < max_dist) {
-                    occluded = true;
-                    break;
-                }
-            }
-        }
-    }
+    Hit unused;
+    walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     return occluded;
 }
 
@@ -309,11 +358,11 @@ struct Seg {
     int depth;
 };
 
-// LIFO of deferred refraction children.  A workgroup is one wave, so for CAP <= 7 the
+// LIFO of deferred refraction children.  A workgroup is one wave, so for CAP <= 4 the
 // stack lives in LDS laid out [entry][field][lane]: every push/pop is 8 lane-contiguous
 // ds_write_b32/ds_read_b32 (conflict-free), and no VGPRs hold waiting segments.  Deeper
-// trees (max_depth > 8) use a private array.
-constexpr int LDS_STACK_MAX = 7;
+// trees (max_depth > 5) use a private array (LDS is kept for 16 resident waves per CU).
+constexpr int LDS_STACK_MAX = 4;
 
 template <int CAP>
 constexpr int lds_stack_floats() { return (CAP >= 1 && CAP <= LDS_STACK_MAX) ? CAP * 8 * 64 : 1; }
@@ -354,8 +403,9 @@ struct DeferStack<CAP, false> {
     __device__ __forceinline__ Seg pop() { return s[--n]; }
 };
 
-template <int CAP, bool COUNT>
-__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt, float* lds) {
+template <int CAP, bool COUNT, bool MESH>
+__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt, float* lds,
+                                       float4* slab) {
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
     DeferStack<CAP> stk(lds);
@@ -363,7 +413,7 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
     for (;;) {
         if (COUNT && cur.depth > 0) ++cnt.sec;
         Hit h;
-        scene_intersect<COUNT>(A, cur.o, cur.d, h, cnt);
+        scene_intersect<COUNT, MESH>(A, cur.o, cur.d, h, cnt, slab);
         bool have_next = false;
         Seg next;
         if (h.kind == HIT_NONE) {
@@ -427,7 +477,7 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
                 float dist = length3(sub(L, p));
                 f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
                 if (COUNT) ++cnt.sh;
-                if (shadow_intersect<COUNT>(A, so, ld, dist, cnt)) continue;
+                if (shadow_intersect<COUNT, MESH>(A, so, ld, dist, cnt, slab)) continue;
                 float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
                 diffuse = add(diffuse, muls(kdv, diff));
                 f3 rdir = reflect3(neg(ld), n);
@@ -537,9 +587,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 }
 
 // One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.
-template <int CAP, bool COUNT>
-__device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds) {
+template <int CAP, bool COUNT, bool MESH>
+__device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
     const uint32_t lane = threadIdx.x;
+    if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;
@@ -553,7 +604,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     f3 acc = mk(0.0f, 0.0f, 0.0f);
     for (uint32_t s = 0; s < spp; ++s) {
         f3 d = primary_dir(A, x, y, s);
-        f3 c = cast_ray<CAP, COUNT>(A, orig, d, cnt, lds);
+        f3 c = cast_ray<CAP, COUNT, MESH>(A, orig, d, cnt, lds, slab);
         acc = (spp == 1u) ? c : add(acc, c);
     }
     cnt.pri += spp;
@@ -572,25 +623,50 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     }
 }
 
+// Blocks b and b+8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md): give each XCD
+// 2x2-tile chunks (16x16 px) so neighbouring pixels' envmap texels and batch records hit
+// the same XCD L2.  Chunk c of XCD x is global chunk c*8+x; chunks are row-major over the
+// image in 2x2 tile units.  Bijective on [0, ntiles) (tail tiles map to themselves).
+__device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
+    const uint32_t tyn = A.ntiles / A.ntx;
+    const uint32_t cw = A.ntx / 2u, ch = tyn / 2u;                 // whole 2x2 chunks
+    const uint32_t nchunk = cw * ch, nfull = (nchunk / 8u) * 8u;   // dealt evenly to the XCDs
+    auto chunk_tile = [&](uint32_t chunk, uint32_t sub) {
+        const uint32_t cx = chunk % cw, cy = chunk / cw;
+        return (cy * 2u + sub / 2u) * A.ntx + cx * 2u + (sub % 2u);
+    };
+    if (b < nfull * 4u) {
+        const uint32_t j = b / 8u, x = b % 8u; // j-th block of XCD x
+        return chunk_tile((j / 4u) * 8u + x, j % 4u);
+    }
+    // leftovers: the last nchunk % 8 chunks, then the odd right column, then the odd bottom row
+    uint32_t r = b - nfull * 4u;
+    const uint32_t nc = (nchunk - nfull) * 4u;
+    if (r < nc) return chunk_tile(nfull + r / 4u, r % 4u);
+    r -= nc;
+    const uint32_t na = (A.ntx & 1u) ? ch * 2u : 0u;
+    if (r < na) return r * A.ntx + (A.ntx - 1u);
+    r -= na;
+    return (ch * 2u) * A.ntx + r; // tile rows odd: the last tile row
+}
+
 // One 64-lane workgroup per 8x8 tile.  The hardware dispatcher hands each freed wave slot
 // the next tile, which balances the very uneven per-tile cost (sky vs. glass sphere) with
 // no atomics.  (Measured on C2: a persistent grid pulling tiles from per-XCD atomic queue
 // heads was 1.5-4.5x slower — 12,288 dequeues per ~60 us frame saturate the heads — and a
 // static grid-stride over the resident waves 1.2-2x slower from imbalance.)
-template <int CAP, bool COUNT>
+// MESH = false is the build for triangle-free scenes (spheres/floor only, e.g. C1/C2): the
+// batch walk is compiled out, which keeps it at 4 waves per SIMD.
+template <int CAP, bool COUNT, bool MESH>
 __global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
+    __shared__ float4 slab[MESH ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
     Cnt cnt;
-#ifdef TRT_TPW
-    for (uint32_t t = blockIdx.x * TRT_TPW; t < min(A.ntiles, (blockIdx.x + 1) * TRT_TPW); ++t)
-        trace_tile<CAP, COUNT>(A, t, cnt, lds);
-#else
-    trace_tile<CAP, COUNT>(A, blockIdx.x, cnt, lds);
-#endif
+    trace_tile<CAP, COUNT, MESH>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
     if (COUNT) {
-        const uint32_t v[9] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt};
+        const uint32_t v[10] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt};
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
+        for (int i = 0; i < 10; ++i) {
             unsigned long long w = wave_sum((unsigned long long)v[i]);
             if (threadIdx.x == 0) atomicAdd(&A.counters[i], w);
         }
@@ -606,10 +682,16 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
 #else
     const dim3 grid(A.ntiles), block(64);
 #endif
-#define TRT_LAUNCH(CAP)                                                                      \
-    do {                                                                                     \
-        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true>), grid, block, 0, stream, A); \
-        else hipLaunchKernelGGL((trace_kernel<CAP, false>), grid, block, 0, stream, A);      \
+    const bool mesh = A.nbatch > 0;
+#define TRT_LAUNCH(CAP)                                                                             \
+    do {                                                                                            \
+        if (mesh) {                                                                                 \
+            if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, true>), grid, block, 0, stream, A);  \
+            else hipLaunchKernelGGL((trace_kernel<CAP, false, true>), grid, block, 0, stream, A);       \
+        } else {                                                                                    \
+            if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, false>), grid, block, 0, stream, A); \
+            else hipLaunchKernelGGL((trace_kernel<CAP, false, false>), grid, block, 0, stream, A);      \
+        }                                                                                           \
     } while (0)
     if (D <= 1) TRT_LAUNCH(0);
     else if (D <= 2) TRT_LAUNCH(1);

@@ -9,7 +9,9 @@
 // and exits, main.cpp:2565-2573).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <limits>
 #include <cstring>
 #include <map>
 #include <new>
@@ -38,6 +40,9 @@ struct trt_ctx {
     bool have_scene = false;
 
     BatchRec* d_batches = nullptr;
+    float4* d_nodes = nullptr; // implicit 8-ary hierarchy over the batches
+    uint32_t node_off[11] = {0};
+    uint32_t top = 0;
     TriGeo* d_geo = nullptr;
     TriShade* d_shade = nullptr;
     Mat* d_mats = nullptr;
@@ -76,11 +81,14 @@ int hip_fail(trt_ctx* c, hipError_t e, const char* what) {
 
 void free_scene(trt_ctx* c) {
     (void)hipFree(c->d_batches);
+    (void)hipFree(c->d_nodes);
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade);
     (void)hipFree(c->d_mats);
     (void)hipFree(c->d_env);
     c->d_batches = nullptr;
+    c->d_nodes = nullptr;
+    c->top = 0;
     c->d_geo = nullptr;
     c->d_shade = nullptr;
     c->d_mats = nullptr;
@@ -265,6 +273,48 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         b.start = m.params0.x;
         b.count_ni = (m.params0.y & 0x7fffffff) | (m.params0.z != 0 ? (int32_t)0x80000000 : 0);
     }
+    // Implicit 8-ary range hierarchy: node k of level L is the exact union of the boxes of
+    // batches [k*8^L, (k+1)*8^L).  A NaN coordinate anywhere below makes the node infinite
+    // (always entered), so culling stays conservative for degenerate input.
+    std::vector<float4> nodes;
+    uint32_t node_off[11] = {0};
+    uint32_t top = 0;
+    while (top < 10 && (1ull << (3 * top)) < (unsigned long long)nmodel) ++top;
+    {
+        std::vector<float4> prev_lo(nmodel), prev_hi(nmodel);
+        for (uint32_t i = 0; i < nmodel; ++i) {
+            const BatchRec& b = batches[i];
+            prev_lo[i] = make_float4(b.bmin[0], b.bmin[1], b.bmin[2], 0.0f);
+            prev_hi[i] = make_float4(b.bmax[0], b.bmax[1], b.bmax[2], 0.0f);
+        }
+        const float inf = std::numeric_limits<float>::infinity();
+        for (uint32_t L = 1; L <= top; ++L) {
+            const size_t n = (prev_lo.size() + 7) / 8;
+            node_off[L] = (uint32_t)(nodes.size() / 2);
+            std::vector<float4> lo(n), hi(n);
+            for (size_t k = 0; k < n; ++k) {
+                float4 a = make_float4(inf, inf, inf, 0.0f), z = make_float4(-inf, -inf, -inf, 0.0f);
+                bool bad = false;
+                for (size_t j = 8 * k; j < std::min(prev_lo.size(), 8 * k + 8); ++j) {
+                    const float4 &l = prev_lo[j], &h = prev_hi[j];
+                    bad |= std::isnan(l.x) || std::isnan(l.y) || std::isnan(l.z) || std::isnan(h.x) ||
+                           std::isnan(h.y) || std::isnan(h.z);
+                    a.x = std::min(a.x, l.x); a.y = std::min(a.y, l.y); a.z = std::min(a.z, l.z);
+                    z.x = std::max(z.x, h.x); z.y = std::max(z.y, h.y); z.z = std::max(z.z, h.z);
+                }
+                if (bad) {
+                    a = make_float4(-inf, -inf, -inf, 0.0f);
+                    z = make_float4(inf, inf, inf, 0.0f);
+                }
+                lo[k] = a;
+                hi[k] = z;
+                nodes.push_back(a);
+                nodes.push_back(z);
+            }
+            prev_lo.swap(lo);
+            prev_hi.swap(hi);
+        }
+    }
     std::vector<TriGeo> geo(ntri);
     std::vector<TriShade> shade(ntri);
     std::vector<Mat> mats;
@@ -322,7 +372,9 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         (rc = upload((void**)&c->d_shade, ntri ? shade.data() : nullptr, sizeof(TriShade) * ntri,
                      "upload triangle shading")) != TRT_OK ||
         (rc = upload((void**)&c->d_mats, mats.data(), sizeof(Mat) * mats.size(),
-                     "upload materials")) != TRT_OK) {
+                     "upload materials")) != TRT_OK ||
+        (rc = upload((void**)&c->d_nodes, nodes.empty() ? nullptr : nodes.data(), sizeof(float4) * nodes.size(),
+                     "upload batch hierarchy")) != TRT_OK) {
         free_scene(c);
         return rc;
     }
@@ -335,6 +387,8 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         c->env_h = env_h;
     }
     c->nbatch = nmodel;
+    c->top = top;
+    std::memcpy(c->node_off, node_off, sizeof(node_off));
     c->ntri = ntri;
     c->nmat = (uint32_t)mats.size();
     c->ubo = *ubo;
@@ -386,6 +440,9 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.env_w = c->env_w;
     A.env_h = c->env_h;
     A.counters = c->d_counters;
+    A.nodes = c->d_nodes;
+    A.top = c->top;
+    std::memcpy(A.node_off, c->node_off, sizeof(A.node_off));
     A.ntx = (A.width + 7u) / 8u;
     A.ntiles = A.ntx * ((A.rows + 7u) / 8u);
 }
@@ -504,6 +561,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
         st->batch_tests = cnt[6];
         st->batch_hits = cnt[7];
         st->tri_tests = cnt[8];
+        st->node_tests = cnt[9];
         st->kernel_ms = 0.0;
         if (timing) {
             float ms = 0.0f;

@@ -101,11 +101,16 @@ class Stats(ctypes.Structure):
         ("batch_tests", ctypes.c_uint64),
         ("batch_hits", ctypes.c_uint64),
         ("tri_tests", ctypes.c_uint64),
+        ("node_tests", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double),
     ]
 
     COUNTERS = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
-                "sphere_tests", "batch_tests", "batch_hits", "tri_tests")
+                "sphere_tests", "batch_tests", "batch_hits", "tri_tests", "node_tests")
+    # counters that must equal the oracle's (the reference's work); batch_tests / node_tests
+    # depend on the traversal (the kernel culls with a conservative hierarchy)
+    EXACT = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
+             "sphere_tests", "batch_hits", "tri_tests")
 
     def as_dict(self) -> dict:
         d = {k: int(getattr(self, k)) for k in self.COUNTERS}
@@ -113,7 +118,7 @@ class Stats(ctypes.Structure):
         return d
 
 
-assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 80
+assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 88
 
 
 def make_params(
