@@ -53,12 +53,13 @@ WORKLOADS = {
 
 
 def algorithmic_bytes(st: dict, pixels: int, envmap: bool) -> int:
-    """SURVEY.md §8(d) units: 24 B per batch bbox tested (+8 B start/count when it passes),
+    """SURVEY.md §8(d) units: 24 B per batch (or hierarchy-node) bbox tested (+8 B start/count
+    when a batch passes),
     36 B per triangle tested (v0, e1, e2), 16 B per sphere tested, 16 B per envmap sample
     (4 RGBA8 texels), 48 B material per closest hit (+36 B vertex normals for a triangle),
     4 B written per pixel."""
     hits = st["primary_rays"] + st["secondary_rays"] - st["misses"]
-    return (24 * st["batch_tests"] + 8 * st["batch_hits"] + 36 * st["tri_tests"]
+    return (24 * (st["batch_tests"] + st.get("node_tests", 0)) + 8 * st["batch_hits"] + 36 * st["tri_tests"]
             + 16 * st["sphere_tests"] + (16 * st["misses"] if envmap else 0)
             + 48 * hits + 36 * st["tri_nearest"] + 4 * pixels)
 
