@@ -54,6 +54,10 @@ extern "C" {
 #define TRT_FLAG_DEVICE_PTRS (1u << 5) /* out_rgba8 / out_rgba32f / rays_in are device pointers */
 #define TRT_FLAG_COUNT (1u << 6)       /* fill trt_stats ray counters */
 #define TRT_FLAG_TIMING (1u << 7)      /* fill trt_stats.kernel_ms (waits for the frame) */
+#define TRT_FLAG_BATCH_WALK (1u << 8)  /* trace meshes by walking the batch list in the reference's
+                                          order (shader.comp:338) instead of the per-ray BVH; same
+                                          image, and batch/triangle work counters equal the
+                                          reference's */
 
 /* The shipped shader: floor on, spheres off, envmap background, host ray quirk. */
 #define TRT_FLAGS_REFERENCE (TRT_FLAG_FLOOR | TRT_FLAG_ENVMAP | TRT_FLAG_ROW_QUIRK)

@@ -15,16 +15,25 @@ pytestmark = pytest.mark.gpu
 SMALL_ENV = (1024, 512)
 
 
-def _counts(st):
-    return tuple(st[k] for k in T.Stats.EXACT)
+def _counts(st, keys=T.Stats.EXACT):
+    return tuple(st[k] for k in keys)
 
 
 def _check(r, sc, params=None, want32=True, max_frac=0.02):
+    """Kernel vs oracle; for mesh scenes both the per-ray BVH (default) and the
+    reference-order batch walk (TRT_FLAG_BATCH_WALK) must match, the walk also in its
+    batch/triangle work counters."""
     p = params if params is not None else sc.params()
     r.upload_scene(sc)
     g8, g32, gst = r.draw_frame(p, want32=want32, count=True)
     o8, o32, ost = orc.render(sc, p, want32=want32)
     assert _counts(gst) == _counts(ost), (gst, ost)
+    if len(sc.models):
+        pw = T.Params.from_buffer_copy(p)
+        pw.flags |= T.FLAG_BATCH_WALK
+        w8, w32, wst = r.draw_frame(pw, want32=want32, count=True)
+        assert _counts(wst, T.Stats.EXACT_WALK) == _counts(ost, T.Stats.EXACT_WALK), (wst, ost)
+        assert np.array_equal(w8, g8) and (not want32 or np.array_equal(w32, g32))
     rep = assert_rgba8_close(g8, o8, max_frac=max_frac)
     if want32:
         assert_float_close(g32, o32)
@@ -223,3 +232,34 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
         gpu_renderer.update_ubo(ubos[i])
         one, _, _ = gpu_renderer.draw_frame(sc.params())
         assert np.array_equal(out[i].cpu().numpy(), one)
+
+
+def test_duplicate_triangles_first_batch_wins(gpu_renderer):
+    """Two copies of one mesh at the same place with different materials: every hit is a t
+    tie, and the reference's strict `t < nearest` (shader.comp:349) keeps the copy in the
+    earlier batch.  Exercises the BVH's (t, batch, triangle) tie-break."""
+    pos, idx = S.icosphere(2)
+    b = S.SceneBuilder()
+    b.add_mesh(pos, idx, S.GLASS_MESH_MAT, scale=(2, 2, 2), translation=(0.5, -1, -9), normal_interp=1)
+    b.add_mesh(pos, idx, S.DRAGON_MAT, scale=(2, 2, 2), translation=(0.5, -1, -9), normal_interp=0)
+    tris, models = b.arrays()
+    sc = S.Scene("dup", S.make_ubo(), tris, models, S.cached_envmap(*SMALL_ENV), 96, 72, 6,
+                 flags=T.FLAG_FLOOR | T.FLAG_ENVMAP | T.FLAG_ROW_QUIRK)
+    _check(gpu_renderer, sc)
+
+
+def test_overlapping_batches_fall_back_to_walk(gpu_renderer):
+    """Model records whose triangle ranges overlap (possible through the ABI, never built by
+    the reference's host code): no BVH is built, the batch walk runs, results match."""
+    pos, idx = S.icosphere(2)
+    b = S.SceneBuilder()
+    b.add_mesh(pos, idx, S.ICE_MAT, scale=(1.5, 1.5, 1.5), translation=(-1, -1, -8), normal_interp=1)
+    tris, models = b.arrays()
+    extra = models[:2].copy()
+    extra["params0"][:, 0] = (10, 40)
+    extra["params0"][:, 1] = (60, 60)
+    extra["material"] = S.RED_RUBBER
+    models = np.concatenate([models, extra])
+    sc = S.Scene("overlap", S.make_ubo(), tris, models, S.cached_envmap(*SMALL_ENV), 80, 60, 5,
+                 flags=T.FLAG_FLOOR | T.FLAG_ENVMAP | T.FLAG_ROW_QUIRK)
+    _check(gpu_renderer, sc)

@@ -1,0 +1,244 @@
+// bvh_build.cpp — binned-SAH BVH2 over the triangles of the uploaded batches.
+//
+// The reference tests every batch box and then every triangle of the batches it enters, in
+// index order (shader.comp:338-361).  For incoherent secondary rays the wave-coherent batch
+// walk pays for the union of the batches 64 lanes enter, so mesh scenes are traced per lane
+// through this BVH instead.  The BVH is culling only — the kernel reproduces the reference's
+// decision exactly:
+//   * a triangle candidate counts only if ray_aabb_intersect of ITS batch box passes (the same
+//     slab test the reference gates the triangle loop with);
+//   * ties in t are broken by (batch, triangle) index, i.e. the first candidate in the
+//     reference's loop order wins, as with its strict `t < nearest` update;
+//   * node boxes are the triangles' exact bounds padded by max(1e-4 * extent, 1e-5 * |coord|,
+//     1e-6) per axis, a margin far above MT / slab rounding, so neither a box miss nor the
+//     distance pruning (skip a node entered beyond the best t) can drop a candidate the
+//     reference would have taken.
+// Built only when the batch ranges are disjoint (each triangle in at most one batch, true for
+// every scene the reference's host code builds); otherwise the batch walk is used.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "../../include/trt/abi.h"
+#include "trt_device.h"
+
+namespace trt {
+
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+    void reset() {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::numeric_limits<float>::infinity();
+            hi[k] = -std::numeric_limits<float>::infinity();
+        }
+    }
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    float area() const {
+        float d[3];
+        for (int k = 0; k < 3; ++k) d[k] = std::max(0.0f, hi[k] - lo[k]);
+        return 2.0f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+};
+
+struct Prim {
+    Box box;
+    float c[3]; // centroid
+    uint32_t tri, batch, ni;
+};
+
+struct Builder {
+    std::vector<Prim> prims;
+    std::vector<BvhNode> nodes;
+    std::vector<uint32_t> order;
+
+    // Returns the child reference (node index, or leaf encoding) for prims [b, e).
+    uint32_t build(uint32_t b, uint32_t e, Box& out_box, int depth) {
+        Box bb, cb;
+        bb.reset();
+        cb.reset();
+        for (uint32_t i = b; i < e; ++i) {
+            bb.grow(prims[i].box);
+            Box c{{prims[i].c[0], prims[i].c[1], prims[i].c[2]}, {prims[i].c[0], prims[i].c[1], prims[i].c[2]}};
+            cb.grow(c);
+        }
+        out_box = bb;
+        const uint32_t n = e - b;
+        if (n <= kBvhLeafMin) return make_leaf(b, e);
+        const bool median_only = depth >= kBvhSahDepth; // bounds the depth: <= 32 + log2(n) levels
+        // binned SAH over the widest centroid axis
+        int axis = 0;
+        float ext = cb.hi[0] - cb.lo[0];
+        for (int k = 1; k < 3; ++k)
+            if (cb.hi[k] - cb.lo[k] > ext) {
+                ext = cb.hi[k] - cb.lo[k];
+                axis = k;
+            }
+        uint32_t mid = b + n / 2;
+        if (ext > 0.0f && !median_only) {
+            constexpr int NB = 16;
+            Box bins[NB];
+            uint32_t cnt[NB] = {0};
+            for (auto& x : bins) x.reset();
+            const float scale = NB / ext;
+            auto bin_of = [&](const Prim& p) {
+                int k = (int)((p.c[axis] - cb.lo[axis]) * scale);
+                return std::min(NB - 1, std::max(0, k));
+            };
+            for (uint32_t i = b; i < e; ++i) {
+                int k = bin_of(prims[i]);
+                bins[k].grow(prims[i].box);
+                cnt[k]++;
+            }
+            float best = std::numeric_limits<float>::infinity();
+            int best_k = -1;
+            Box left;
+            left.reset();
+            uint32_t nl = 0;
+            for (int k = 0; k < NB - 1; ++k) {
+                left.grow(bins[k]);
+                nl += cnt[k];
+                Box right;
+                right.reset();
+                uint32_t nr = 0;
+                for (int m = k + 1; m < NB; ++m) {
+                    right.grow(bins[m]);
+                    nr += cnt[m];
+                }
+                if (!nl || !nr) continue;
+                const float cost = left.area() * nl + right.area() * nr;
+                if (cost < best) {
+                    best = cost;
+                    best_k = k;
+                }
+            }
+            const float leaf_cost = bb.area() * n;
+            if (n <= kBvhLeafMax && !(best < leaf_cost)) return make_leaf(b, e);
+            if (best_k >= 0) {
+                auto it = std::partition(prims.begin() + b, prims.begin() + e,
+                                         [&](const Prim& p) { return bin_of(p) <= best_k; });
+                mid = (uint32_t)(it - prims.begin());
+                if (mid == b || mid == e) mid = b + n / 2;
+            }
+        }
+        if (mid == b + n / 2) {
+            std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e,
+                             [&](const Prim& x, const Prim& y) { return x.c[axis] < y.c[axis]; });
+        }
+        const uint32_t idx = (uint32_t)nodes.size();
+        nodes.emplace_back();
+        Box lb, rb;
+        const uint32_t l = build(b, mid, lb, depth + 1);
+        const uint32_t r = build(mid, e, rb, depth + 1);
+        BvhNode& nd = nodes[idx];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo0[k] = lb.lo[k];
+            nd.hi0[k] = lb.hi[k];
+            nd.lo1[k] = rb.lo[k];
+            nd.hi1[k] = rb.hi[k];
+        }
+        nd.child[0] = l;
+        nd.child[1] = r;
+        return idx;
+    }
+
+    uint32_t make_leaf(uint32_t b, uint32_t e) { // 1 <= e - b <= kBvhLeafMax
+        const uint32_t start = (uint32_t)order.size();
+        for (uint32_t i = b; i < e; ++i) order.push_back(i);
+        return kBvhLeafBit | ((e - b - 1u) << kBvhCountShift) | start;
+    }
+};
+
+Box tri_box(const trt_triangle& t) {
+    Box b;
+    const trt_vec4* v[3] = {&t.v0, &t.v1, &t.v2};
+    for (int k = 0; k < 3; ++k) {
+        float lo = std::numeric_limits<float>::infinity(), hi = -lo;
+        for (int m = 0; m < 3; ++m) {
+            const float c = (&v[m]->x)[k];
+            lo = std::min(lo, c);
+            hi = std::max(hi, c);
+        }
+        const float pad = std::max({1e-4f * (hi - lo), 1e-5f * std::max(std::fabs(lo), std::fabs(hi)), 1e-6f});
+        b.lo[k] = lo - pad;
+        b.hi[k] = hi + pad;
+    }
+    return b;
+}
+
+} // namespace
+
+// Returns false (no BVH) when batch ranges overlap, a triangle is NaN, or nothing is covered.
+bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
+               std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris) {
+    nodes.clear();
+    leaf_tris.clear();
+    std::vector<int32_t> owner(ntri, -1);
+    for (uint32_t i = 0; i < nmodel; ++i) {
+        const int32_t s = models[i].params0.x, n = models[i].params0.y;
+        for (int32_t j = s; j < s + n; ++j) {
+            if (owner[j] >= 0) return false; // overlapping batches: keep the batch walk
+            owner[j] = (int32_t)i;
+        }
+    }
+    Builder B;
+    for (uint32_t j = 0; j < ntri; ++j) {
+        if (owner[j] < 0) continue; // never tested by the reference
+        const trt_triangle& t = tris[j];
+        for (const trt_vec4* v : {&t.v0, &t.v1, &t.v2})
+            if (std::isnan(v->x) || std::isnan(v->y) || std::isnan(v->z)) return false;
+        Prim p;
+        p.box = tri_box(t);
+        for (int k = 0; k < 3; ++k) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
+        p.tri = j;
+        p.batch = (uint32_t)owner[j];
+        p.ni = models[owner[j]].params0.z != 0 ? 1u : 0u;
+        B.prims.push_back(p);
+    }
+    if (B.prims.empty()) return false;
+    B.nodes.reserve(2 * B.prims.size() / kBvhLeafMin + 2);
+    Box root;
+    const uint32_t r = B.build(0, (uint32_t)B.prims.size(), root, 0);
+    if (r & kBvhLeafBit) { // single leaf: wrap it in a node with an empty second child
+        BvhNode nd;
+        for (int k = 0; k < 3; ++k) {
+            nd.lo0[k] = root.lo[k];
+            nd.hi0[k] = root.hi[k];
+            nd.lo1[k] = 1.0f;
+            nd.hi1[k] = -1.0f; // empty box: never entered
+        }
+        nd.child[0] = r;
+        nd.child[1] = r;
+        B.nodes.insert(B.nodes.begin(), nd);
+    }
+    nodes.swap(B.nodes);
+    leaf_tris.resize(B.order.size());
+    for (size_t k = 0; k < B.order.size(); ++k) {
+        const Prim& p = B.prims[B.order[k]];
+        const trt_triangle& t = tris[p.tri];
+        TriGeo& g = leaf_tris[k];
+        g.v0[0] = t.v0.x;
+        g.v0[1] = t.v0.y;
+        g.v0[2] = t.v0.z;
+        g.e1[0] = t.v1.x - t.v0.x; // the shader's own subtraction (shader.comp:230-231)
+        g.e1[1] = t.v1.y - t.v0.y;
+        g.e1[2] = t.v1.z - t.v0.z;
+        g.e2[0] = t.v2.x - t.v0.x;
+        g.e2[1] = t.v2.y - t.v0.y;
+        g.e2[2] = t.v2.z - t.v0.z;
+        uint32_t meta[3] = {p.tri, p.batch, p.ni};
+        std::memcpy(g.pad, meta, sizeof(meta));
+    }
+    return true;
+}
+
+} // namespace trt

@@ -44,6 +44,22 @@ struct alignas(16) TriShade {
 };
 static_assert(sizeof(TriShade) == 48, "TriShade is 3 x dwordx4");
 
+// BVH2 node over triangles (bvh_build.cpp): both children's boxes live in the parent, so a
+// visit is one 64 B load and two slab tests.  child[k]: node index, or a leaf
+// (kBvhLeafBit | (count - 1) << kBvhCountShift | first) into the BVH-ordered triangle array.
+constexpr uint32_t kBvhLeafBit = 0x80000000u;
+constexpr uint32_t kBvhCountShift = 27u;
+constexpr uint32_t kBvhFirstMask = (1u << kBvhCountShift) - 1u;
+constexpr uint32_t kBvhLeafMin = 4u, kBvhLeafMax = 8u;
+constexpr int kBvhSahDepth = 32;  // below this depth only median splits
+constexpr int kBvhStack = 64;     // traversal stack >= max depth (32 + log2(2^27))
+struct alignas(16) BvhNode {
+    float lo0[3], hi0[3], lo1[3], hi1[3];
+    uint32_t child[2];
+    uint32_t pad[2];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
+
 struct Mat {
     float albedo[4];
     float kd[3];
@@ -81,6 +97,8 @@ struct KArgs {
     uint32_t* __restrict__ out8;       // packed RGBA8, or null
     float* __restrict__ out32;         // float4 per pixel, or null
     unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
+    const BvhNode* __restrict__ bvh;  // per-lane BVH over triangles, or null (batch walk)
+    const TriGeo* __restrict__ bvh_tris; // BVH-ordered geometry; pad = (triangle, batch, ni)
     const float4* __restrict__ nodes; // batch hierarchy: per node (lo.xyz, -), (hi.xyz, -)
     uint32_t node_off[11];            // first node of level L (L = 1..top) in `nodes`
     uint32_t top;                     // levels above the batches: 8^top >= nbatch

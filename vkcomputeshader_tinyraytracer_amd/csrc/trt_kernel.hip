@@ -124,7 +124,8 @@ struct Hit {
     int kind;
     int idx; // sphere index or triangle index
     float u, v;
-    int ni; // normal interpolation flag of the batch that produced the triangle hit
+    int ni;       // normal interpolation flag of the batch that produced the triangle hit
+    uint32_t batch; // that batch (BVH tie-break on (t, batch, triangle))
 };
 
 // ---- batch walk: implicit 8-ary range hierarchy + the reference batch test -----------------
@@ -249,7 +250,112 @@ __device__ __forceinline__ void walk_batches(const KArgs& A, f3 o, f3 d, f3 inv,
     }
 }
 
-template <bool COUNT, bool MESH>
+// ---- per-lane BVH traversal (bvh_build.cpp) ----------------------------------------------
+//
+// Each lane walks the BVH2 on its own (ordered: nearer child first, farther child on a private
+// stack), which suits incoherent refracted / shadow rays far better than the wave-wide batch
+// walk.  The result is the reference's: a triangle candidate (MT hit, t > MIN_EPSILON) is
+// accepted only if its batch passes ray_aabb_intersect exactly as in shader.comp:339, and it
+// replaces the current best only if t is smaller or t is equal and (batch, triangle) comes
+// first in the reference's loop order (its strict `t < nearest` keeps the first candidate).
+
+// Padded-box entry test with distance pruning: enter if the slab interval is non-empty, ends
+// beyond MIN_EPSILON, and starts no later than `best`.  NaN slabs are unconstrained.
+__device__ __forceinline__ bool bvh_box(f3 o, f3 inv, const float* lo, const float* hi, float best,
+                                        float& tnear) {
+    const float INF = __builtin_huge_valf();
+    float t0x = (lo[0] - o.x) * inv.x, t1x = (hi[0] - o.x) * inv.x;
+    float t0y = (lo[1] - o.y) * inv.y, t1y = (hi[1] - o.y) * inv.y;
+    float t0z = (lo[2] - o.z) * inv.z, t1z = (hi[2] - o.z) * inv.z;
+    const bool nx = (t0x != t0x) || (t1x != t1x);
+    const bool ny = (t0y != t0y) || (t1y != t1y);
+    const bool nz = (t0z != t0z) || (t1z != t1z);
+    const float mnx = nx ? -INF : fminf(t0x, t1x), mxx = nx ? INF : fmaxf(t0x, t1x);
+    const float mny = ny ? -INF : fminf(t0y, t1y), mxy = ny ? INF : fmaxf(t0y, t1y);
+    const float mnz = nz ? -INF : fminf(t0z, t1z), mxz = nz ? INF : fmaxf(t0z, t1z);
+    tnear = fmaxf(fmaxf(mnx, mny), mnz);
+    const float tfar = fminf(fminf(mxx, mxy), mxz);
+    return tnear <= tfar && tfar > TRT_EPS && tnear <= best;
+}
+
+template <bool COUNT, bool SHADOW>
+__device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
+                                          float max_dist, Cnt& c) {
+    uint32_t stack[kBvhStack];
+    int sp = 0;
+    uint32_t node = 0;
+    float best = SHADOW ? max_dist : h.t;
+    for (;;) {
+        if (!(node & kBvhLeafBit)) {
+            const BvhNode nd = A.bvh[node];
+            float ta, tb;
+            const bool ha = bvh_box(o, inv, nd.lo0, nd.hi0, best, ta);
+            const bool hb = bvh_box(o, inv, nd.lo1, nd.hi1, best, tb);
+            if (COUNT) c.nt += 2;
+            if (ha && hb) {
+                const bool a_first = ta <= tb;
+                stack[sp++] = a_first ? nd.child[1] : nd.child[0];
+                node = a_first ? nd.child[0] : nd.child[1];
+                continue;
+            }
+            if (ha || hb) {
+                node = ha ? nd.child[0] : nd.child[1];
+                continue;
+            }
+        } else {
+            const uint32_t first = node & kBvhFirstMask;
+            const uint32_t n = ((node >> kBvhCountShift) & 15u) + 1u;
+            for (uint32_t k = first; k < first + n; ++k) {
+                const TriGeo g = A.bvh_tris[k];
+                if (COUNT) ++c.tt;
+                const f3 v0 = ld3(g.v0), e1 = ld3(g.e1), e2 = ld3(g.e2);
+                f3 hv = cross3(d, e2);
+                float a = dot3(e1, hv);
+                if (a > -TRT_EPS && a < TRT_EPS) continue;
+                float f = 1.0f / a;
+                f3 sv = sub(o, v0);
+                float u = f * dot3(sv, hv);
+                if (u < 0.0f || u > 1.0f) continue;
+                f3 q = cross3(sv, e1);
+                float v = f * dot3(d, q);
+                if (v < 0.0f || u + v > 1.0f) continue;
+                float t = f * dot3(e2, q);
+                if (t <= TRT_EPS) continue;
+                const uint32_t tri = __float_as_uint(g.pad[0]), batch = __float_as_uint(g.pad[1]);
+                if (SHADOW) {
+                    if (!(t < max_dist)) continue;
+                } else {
+                    const bool better = t < best || (t == best && h.kind == HIT_TRI &&
+                                                     (batch < h.batch || (batch == h.batch && (int)tri < h.idx)));
+                    if (!better) continue;
+                }
+                const BatchRec rec = A.batches[batch]; // the reference's gate for this triangle
+                const bool pass = aabb_hit(o, inv, rec.bmin, rec.bmax);
+                if (COUNT) {
+                    ++c.bt;
+                    c.bh += pass ? 1u : 0u;
+                }
+                if (!pass) continue;
+                if (SHADOW) {
+                    occluded = true;
+                    return;
+                }
+                best = t;
+                h.t = t;
+                h.kind = HIT_TRI;
+                h.idx = (int)tri;
+                h.batch = batch;
+                h.u = u;
+                h.v = v;
+                h.ni = (int)__float_as_uint(g.pad[2]);
+            }
+        }
+        if (sp == 0) return;
+        node = stack[--sp];
+    }
+}
+
+template <bool COUNT, int GEOM>
 __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit& h, Cnt& c, float4* slab) {
     h.t = 1e10f;
     h.kind = HIT_NONE;
@@ -257,6 +363,7 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
     h.u = 0.0f;
     h.v = 0.0f;
     h.ni = 0;
+    h.batch = 0;
     if (A.flags & TRT_FLAG_FLOOR) { // shader.comp:302-320
         if (fabsf(d.y) > TRT_EPS) {
             float t = -(o.y + 4.0f) / d.y;
@@ -281,14 +388,15 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
             }
         }
     }
-    if (!MESH || A.nbatch == 0) return;
+    if (GEOM == 0 || A.nbatch == 0) return;
     f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:336
     bool unused = false;
-    walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
+    if (GEOM == 2) trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c);
+    else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
 }
 
 // shadow_intersect, shader.comp:364-399: any hit on spheres / triangles; floor excluded.
-template <bool COUNT, bool MESH>
+template <bool COUNT, int GEOM>
 __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, float max_dist, Cnt& c,
                                                  float4* slab) {
 #ifdef TRT_DIAG_NO_SHADOW
@@ -302,11 +410,12 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
             if (sphere_hit(o, d, A.sph[i], t) && t < max_dist) return true;
         }
     }
-    if (!MESH || A.nbatch == 0) return false;
+    if (GEOM == 0 || A.nbatch == 0) return false;
     f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:377
     bool occluded = false;
     Hit unused;
-    walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+    if (GEOM == 2) trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c);
+    else walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     return occluded;
 }
 
@@ -403,7 +512,7 @@ struct DeferStack<CAP, false> {
     __device__ __forceinline__ Seg pop() { return s[--n]; }
 };
 
-template <int CAP, bool COUNT, bool MESH>
+template <int CAP, bool COUNT, int GEOM>
 __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt, float* lds,
                                        float4* slab) {
     const int D = (int)A.max_depth;
@@ -413,7 +522,7 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
     for (;;) {
         if (COUNT && cur.depth > 0) ++cnt.sec;
         Hit h;
-        scene_intersect<COUNT, MESH>(A, cur.o, cur.d, h, cnt, slab);
+        scene_intersect<COUNT, GEOM>(A, cur.o, cur.d, h, cnt, slab);
         bool have_next = false;
         Seg next;
         if (h.kind == HIT_NONE) {
@@ -477,7 +586,7 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
                 float dist = length3(sub(L, p));
                 f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
                 if (COUNT) ++cnt.sh;
-                if (shadow_intersect<COUNT, MESH>(A, so, ld, dist, cnt, slab)) continue;
+                if (shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab)) continue;
                 float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
                 diffuse = add(diffuse, muls(kdv, diff));
                 f3 rdir = reflect3(neg(ld), n);
@@ -587,7 +696,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 }
 
 // One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.
-template <int CAP, bool COUNT, bool MESH>
+template <int CAP, bool COUNT, int GEOM>
 __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
     const uint32_t lane = threadIdx.x;
     if (tile >= A.ntiles) return;
@@ -604,7 +713,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     f3 acc = mk(0.0f, 0.0f, 0.0f);
     for (uint32_t s = 0; s < spp; ++s) {
         f3 d = primary_dir(A, x, y, s);
-        f3 c = cast_ray<CAP, COUNT, MESH>(A, orig, d, cnt, lds, slab);
+        f3 c = cast_ray<CAP, COUNT, GEOM>(A, orig, d, cnt, lds, slab);
         acc = (spp == 1u) ? c : add(acc, c);
     }
     cnt.pri += spp;
@@ -655,14 +764,14 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
 // no atomics.  (Measured on C2: a persistent grid pulling tiles from per-XCD atomic queue
 // heads was 1.5-4.5x slower — 12,288 dequeues per ~60 us frame saturate the heads — and a
 // static grid-stride over the resident waves 1.2-2x slower from imbalance.)
-// MESH = false is the build for triangle-free scenes (spheres/floor only, e.g. C1/C2): the
-// batch walk is compiled out, which keeps it at 4 waves per SIMD.
-template <int CAP, bool COUNT, bool MESH>
+// GEOM: 0 = no triangles (spheres/floor only, e.g. C1/C2: the triangle code is compiled
+// out, 4 waves per SIMD); 1 = the reference-order batch walk; 2 = per-lane BVH.
+template <int CAP, bool COUNT, int GEOM>
 __global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
-    __shared__ float4 slab[MESH ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
+    __shared__ float4 slab[GEOM == 1 ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
     Cnt cnt;
-    trace_tile<CAP, COUNT, MESH>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
+    trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
     if (COUNT) {
         const uint32_t v[10] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt};
 #pragma unroll
@@ -682,16 +791,17 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
 #else
     const dim3 grid(A.ntiles), block(64);
 #endif
-    const bool mesh = A.nbatch > 0;
-#define TRT_LAUNCH(CAP)                                                                             \
-    do {                                                                                            \
-        if (mesh) {                                                                                 \
-            if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, true>), grid, block, 0, stream, A);  \
-            else hipLaunchKernelGGL((trace_kernel<CAP, false, true>), grid, block, 0, stream, A);       \
-        } else {                                                                                    \
-            if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, false>), grid, block, 0, stream, A); \
-            else hipLaunchKernelGGL((trace_kernel<CAP, false, false>), grid, block, 0, stream, A);      \
-        }                                                                                           \
+    const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? 2 : 1;
+#define TRT_LAUNCH_G(CAP, G)                                                                      \
+    do {                                                                                          \
+        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G>), grid, block, 0, stream, A);   \
+        else hipLaunchKernelGGL((trace_kernel<CAP, false, G>), grid, block, 0, stream, A);        \
+    } while (0)
+#define TRT_LAUNCH(CAP)                          \
+    do {                                         \
+        if (geom == 0) TRT_LAUNCH_G(CAP, 0);     \
+        else if (geom == 1) TRT_LAUNCH_G(CAP, 1); \
+        else TRT_LAUNCH_G(CAP, 2);               \
     } while (0)
     if (D <= 1) TRT_LAUNCH(0);
     else if (D <= 2) TRT_LAUNCH(1);
@@ -701,6 +811,7 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     else if (D <= 8) TRT_LAUNCH(7);
     else TRT_LAUNCH(19);
 #undef TRT_LAUNCH
+#undef TRT_LAUNCH_G
     return hipGetLastError();
 }
 

@@ -23,6 +23,8 @@
 
 namespace trt {
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
+bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
+               std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris);
 }
 
 using trt::BatchRec;
@@ -41,6 +43,8 @@ struct trt_ctx {
 
     BatchRec* d_batches = nullptr;
     float4* d_nodes = nullptr; // implicit 8-ary hierarchy over the batches
+    trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
+    TriGeo* d_bvh_tris = nullptr;
     uint32_t node_off[11] = {0};
     uint32_t top = 0;
     TriGeo* d_geo = nullptr;
@@ -82,12 +86,16 @@ int hip_fail(trt_ctx* c, hipError_t e, const char* what) {
 void free_scene(trt_ctx* c) {
     (void)hipFree(c->d_batches);
     (void)hipFree(c->d_nodes);
+    (void)hipFree(c->d_bvh);
+    (void)hipFree(c->d_bvh_tris);
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade);
     (void)hipFree(c->d_mats);
     (void)hipFree(c->d_env);
     c->d_batches = nullptr;
     c->d_nodes = nullptr;
+    c->d_bvh = nullptr;
+    c->d_bvh_tris = nullptr;
     c->top = 0;
     c->d_geo = nullptr;
     c->d_shade = nullptr;
@@ -378,6 +386,16 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         free_scene(c);
         return rc;
     }
+    std::vector<trt::BvhNode> bvh;
+    std::vector<TriGeo> bvh_tris;
+    if (nmodel && trt::build_bvh(tris, ntri, models, nmodel, bvh, bvh_tris)) {
+        if ((rc = upload((void**)&c->d_bvh, bvh.data(), sizeof(trt::BvhNode) * bvh.size(), "upload bvh")) != TRT_OK ||
+            (rc = upload((void**)&c->d_bvh_tris, bvh_tris.data(), sizeof(TriGeo) * bvh_tris.size(),
+                         "upload bvh triangles")) != TRT_OK) {
+            free_scene(c);
+            return rc;
+        }
+    }
     if (env) {
         if ((rc = upload((void**)&c->d_env, env, (size_t)env_w * env_h * 4, "upload envmap")) != TRT_OK) {
             free_scene(c);
@@ -441,6 +459,8 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.env_h = c->env_h;
     A.counters = c->d_counters;
     A.nodes = c->d_nodes;
+    A.bvh = c->d_bvh;
+    A.bvh_tris = c->d_bvh_tris;
     A.top = c->top;
     std::memcpy(A.node_off, c->node_off, sizeof(A.node_off));
     A.ntx = (A.width + 7u) / 8u;

@@ -57,6 +57,7 @@ FLAG_ROW_QUIRK = 1 << 4
 FLAG_DEVICE_PTRS = 1 << 5
 FLAG_COUNT = 1 << 6
 FLAG_TIMING = 1 << 7
+FLAG_BATCH_WALK = 1 << 8
 FLAGS_REFERENCE = FLAG_FLOOR | FLAG_ENVMAP | FLAG_ROW_QUIRK
 
 MAX_DEPTH_LIMIT = 20
@@ -110,7 +111,9 @@ class Stats(ctypes.Structure):
     # counters that must equal the oracle's (the reference's work); batch_tests / node_tests
     # depend on the traversal (the kernel culls with a conservative hierarchy)
     EXACT = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
-             "sphere_tests", "batch_hits", "tri_tests")
+             "sphere_tests")
+    # with TRT_FLAG_BATCH_WALK the kernel also tests exactly the reference's batches/triangles
+    EXACT_WALK = EXACT + ("batch_hits", "tri_tests")
 
     def as_dict(self) -> dict:
         d = {k: int(getattr(self, k)) for k in self.COUNTERS}
