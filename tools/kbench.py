@@ -53,11 +53,24 @@ def main():
     r.render_frames(p, out, a.frames, timing=True)
     ms = r.frame_times(a.frames)
     torch.cuda.synchronize()
+    # wall per frame of a back-to-back batch without per-frame events (one event pair)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    r.render_frames(p, out, a.frames)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall_noev = e0.elapsed_time(e1) / a.frames
+    e0.record(stream)
+    r.render_frames(p, out, a.frames, timing=True)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall_ev = e0.elapsed_time(e1) / a.frames
     rays = st["primary_rays"] + st["secondary_rays"]
     res = {"tag": a.tag, "sched": os.environ.get("TRT_SCHED", "persistent"), "config": a.config,
            "size": [p.width, p.height], "depth": p.max_depth, "rays": rays,
            "med_us": round(float(np.median(ms)) * 1e3, 2), "min_us": round(float(ms.min()) * 1e3, 2),
-           "Mray_s_kernel": round(rays / (float(np.median(ms)) * 1e-3) / 1e6, 1)}
+           "Mray_s_kernel": round(rays / (float(np.median(ms)) * 1e-3) / 1e6, 1),
+           "wall_us_no_events": round(wall_noev * 1e3, 2), "wall_us_with_events": round(wall_ev * 1e3, 2)}
     print(json.dumps(res), flush=True)
     r.close()
 
