@@ -130,11 +130,14 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * bytes (frame_stride 0 = every frame overwrites the same image).  Requires
  * TRT_FLAG_DEVICE_PTRS; only enqueues.  Host cost per frame is one kernel launch, so
  * back-to-back frames keep the GPU busy.  With TRT_FLAG_TIMING a HIP event pair brackets
- * every launch on the stream; trt_frame_times() reads the per-frame kernel times. */
+ * the launch of every `time_every`-th frame (0 or 1: every frame) on the stream — an event
+ * pair costs a few microseconds of queue time, so a sparse sample keeps a timed frame loop
+ * representative; trt_frame_times() reads the sampled kernel times. */
 int trt_render_frames(trt_ctx* ctx, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
-                      uint8_t* out_rgba8, size_t frame_stride);
+                      uint8_t* out_rgba8, size_t frame_stride, uint32_t time_every);
 
-/* Per-frame device times (ms) of the last timed trt_render_frames call (waits for them). */
+/* Device times (ms) of the frames sampled by the last timed trt_render_frames call (waits
+ * for them); n <= the number of sampled frames. */
 int trt_frame_times(trt_ctx* ctx, float* ms, uint32_t n);
 
 /* Waits for all work enqueued on the context's stream. */

@@ -226,8 +226,15 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
     gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4, timing=True)
     ms = gpu_renderer.frame_times(4)
     torch.cuda.synchronize()
-    gpu_renderer.set_stream(None)
     assert (ms > 0).all()
+    # sampled timing: frames 0 and 3 of 4 are bracketed; asking for more is an error
+    assert gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4,
+                                      timing=True, time_every=3) == 2
+    assert (gpu_renderer.frame_times(2) > 0).all()
+    with pytest.raises(TrtError):
+        gpu_renderer.frame_times(3)
+    torch.cuda.synchronize()
+    gpu_renderer.set_stream(None)
     for i in range(4):
         gpu_renderer.update_ubo(ubos[i])
         one, _, _ = gpu_renderer.draw_frame(sc.params())

@@ -47,7 +47,7 @@ def lib() -> ctypes.CDLL:
         "trt_upload_scene": (c_int, [vp, vp, vp, c_u32, vp, c_u32, vp, c_u32, c_u32]),
         "trt_update_ubo": (c_int, [vp, vp]),
         "trt_render": (c_int, [vp, ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)]),
-        "trt_render_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, vp, ctypes.c_size_t]),
+        "trt_render_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, vp, ctypes.c_size_t, c_u32]),
         "trt_frame_times": (c_int, [vp, ctypes.POINTER(ctypes.c_float), c_u32]),
         "trt_synchronize": (c_int, [vp]),
         "trt_output_rows": (c_u32, [ctypes.POINTER(Params)]),

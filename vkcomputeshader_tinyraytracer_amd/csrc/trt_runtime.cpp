@@ -470,7 +470,7 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
 } // namespace
 
 extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
-                                 uint8_t* out8, size_t frame_stride) {
+                                 uint8_t* out8, size_t frame_stride, uint32_t time_every) {
     if (!c) return TRT_ERR_INVALID;
     int rc = check_params(c, p);
     if (rc != TRT_OK) return rc;
@@ -480,13 +480,15 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
         return fail(c, TRT_ERR_INVALID, "trt_render_frames: COUNT is a per-frame trt_render flag");
     HIP_TRY(c, hipSetDevice(c->device));
     const bool timing = (p->flags & TRT_FLAG_TIMING) != 0;
+    const uint32_t every = time_every ? time_every : 1u;
+    c->fev_frames = 0;
     if (timing) {
-        while (c->fev.size() < 2 * (size_t)nframes) {
+        const uint32_t ntimed = (nframes + every - 1) / every; // frames 0, every, 2*every, ...
+        while (c->fev.size() < 2 * (size_t)ntimed) {
             hipEvent_t e;
             HIP_TRY(c, hipEventCreate(&e));
             c->fev.push_back(e);
         }
-        c->fev_frames = nframes;
     }
     KArgs A;
     fill_args(c, p, A);
@@ -498,9 +500,14 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
             fill_ubo_args(A, c->ubo);
         }
         A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
-        if (timing) HIP_TRY(c, hipEventRecord(c->fev[2 * i], c->stream));
+        const bool timed = timing && i % every == 0;
+        const size_t k = 2 * (size_t)(i / every);
+        if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], c->stream));
         HIP_TRY(c, trt::launch_trace(A, c->stream, false));
-        if (timing) HIP_TRY(c, hipEventRecord(c->fev[2 * i + 1], c->stream));
+        if (timed) {
+            HIP_TRY(c, hipEventRecord(c->fev[k + 1], c->stream));
+            c->fev_frames = i / every + 1;
+        }
     }
     return TRT_OK;
 }

@@ -115,9 +115,12 @@ class Renderer:
         return out8, out32, st.as_dict()
 
     def render_frames(self, params: T.Params, out8, nframes: int, ubos: np.ndarray | None = None,
-                      frame_stride: int = 0, timing: bool = False) -> None:
+                      frame_stride: int = 0, timing: bool = False, time_every: int = 1) -> int:
         """Native frame loop (trt_render_frames): `nframes` launches enqueued back to back on
-        the context's stream into the device tensor `out8` (+ i * frame_stride bytes)."""
+        the context's stream into the device tensor `out8` (+ i * frame_stride bytes).
+
+        With `timing`, frames 0, time_every, 2*time_every, ... are bracketed by HIP events;
+        returns how many were (read them with frame_times)."""
         if not _is_torch_cuda(out8):
             raise ValueError("render_frames renders into a device (torch CUDA) tensor")
         p = T.Params.from_buffer_copy(params)
@@ -135,7 +138,9 @@ class Renderer:
             u = np.ascontiguousarray(ubos, T.UBO)
             assert u.shape[0] >= nframes
         self._check(self._L.trt_render_frames(self._h, ctypes.byref(p), u.ctypes.data if u is not None else None,
-                                              nframes, out8.data_ptr(), frame_stride))
+                                              nframes, out8.data_ptr(), frame_stride, time_every))
+        every = max(1, time_every)
+        return (nframes + every - 1) // every if timing else 0
 
     def frame_times(self, n: int) -> np.ndarray:
         ms = (ctypes.c_float * n)()
