@@ -58,6 +58,10 @@ extern "C" {
                                           order (shader.comp:338) instead of the per-ray BVH; same
                                           image, and batch/triangle work counters equal the
                                           reference's */
+#define TRT_FLAG_SRGB_OUT (1u << 9)    /* out_rgba8 = the frame as displayed: sRGB-encoded
+                                          (the B8G8R8A8_SRGB swapchain, main.cpp:2341, that
+                                          shader.frag writes the sampled image to); out_rgba32f
+                                          stays rayOut */
 
 /* The shipped shader: floor on, spheres off, envmap background, host ray quirk. */
 #define TRT_FLAGS_REFERENCE (TRT_FLAG_FLOOR | TRT_FLAG_ENVMAP | TRT_FLAG_ROW_QUIRK)
@@ -181,6 +185,14 @@ uint32_t trt_scene_triangle_count(const trt_scene* s);
 uint32_t trt_scene_model_count(const trt_scene* s);
 const trt_triangle* trt_scene_triangles(const trt_scene* s);
 const trt_model* trt_scene_models(const trt_scene* s);
+
+/* ---- frame files (the reference only presents, main.cpp:2181-2205) ------- */
+
+/* Binary PPM (P6, RGB; alpha dropped) of a host RGBA8 frame, e.g. trt_render's out_rgba8. */
+int trt_write_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
+
+/* 8-bit RGBA PNG (zlib deflate) of a host RGBA8 frame. */
+int trt_write_png(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -654,6 +654,12 @@ typedef struct {
     _Atomic uint64_t acc[9];
 } job_t;
 
+/* Linear -> sRGB transfer (IEC 61966-2-1) of the B8G8R8A8_SRGB swapchain the reference
+ * presents through (main.cpp:2341; shader.frag samples the RGBA32F image, main.cpp:869). */
+static float srgb_encode(float x) {
+    return x <= 0.0031308f ? 12.92f * x : 1.055f * powf(x, 1.0f / 2.4f) - 0.055f;
+}
+
 static void render_row(job_t* J, uint32_t k, counters* cnt, path_segment* lit_stack) {
     const trt_params* p = J->p;
     uint32_t y = J->rows[k], W = p->width;
@@ -678,9 +684,12 @@ static void render_row(job_t* J, uint32_t k, counters* cnt, path_segment* lit_st
             J->out32[4 * o + 3] = 1.0f;
         }
         if (J->out8) { /* UNORM8 store of the rgba8 image, shader.comp:61, 600 */
-            J->out8[4 * o + 0] = (uint8_t)floorf(g.x * 255.0f + 0.5f);
-            J->out8[4 * o + 1] = (uint8_t)floorf(g.y * 255.0f + 0.5f);
-            J->out8[4 * o + 2] = (uint8_t)floorf(g.z * 255.0f + 0.5f);
+            v3 e = g;
+            if (p->flags & TRT_FLAG_SRGB_OUT) /* as displayed: sRGB swapchain, main.cpp:2341 */
+                e = mk(srgb_encode(g.x), srgb_encode(g.y), srgb_encode(g.z));
+            J->out8[4 * o + 0] = (uint8_t)floorf(e.x * 255.0f + 0.5f);
+            J->out8[4 * o + 1] = (uint8_t)floorf(e.y * 255.0f + 0.5f);
+            J->out8[4 * o + 2] = (uint8_t)floorf(e.z * 255.0f + 0.5f);
             J->out8[4 * o + 3] = 255;
         }
     }

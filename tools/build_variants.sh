@@ -8,7 +8,7 @@ OUT=$ROOT/diag
 mkdir -p "$OUT" "$ROOT/build/diag"
 FP="-ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math -fno-slp-vectorize"
 HOST="-O2 -std=c++17 -fPIC -ffp-contract=off -I/opt/rocm/include -D__HIP_PLATFORM_AMD__"
-for f in trt_runtime scene_build obj_load bvh_build; do
+for f in trt_runtime scene_build obj_load bvh_build image_io; do
     [ "$ROOT/build/diag/$f.o" -nt "$SRC/$f.cpp" ] || /opt/rocm/bin/hipcc $HOST -x c++ -c -o "$ROOT/build/diag/$f.o" "$SRC/$f.cpp"
 done
 variant() { # name extra-flags...
@@ -17,7 +17,7 @@ variant() { # name extra-flags...
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "$@" -c -o "$ROOT/build/diag/k_$name.o" "$SRC/trt_kernel.hip"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libtrt_$name.so" "$ROOT/build/diag/k_$name.o" \
         "$ROOT/build/diag/trt_runtime.o" "$ROOT/build/diag/scene_build.o" "$ROOT/build/diag/obj_load.o" \
-        "$ROOT/build/diag/bvh_build.o"
+        "$ROOT/build/diag/bvh_build.o" "$ROOT/build/diag/image_io.o" -lz
     echo "built $OUT/libtrt_$name.so"
 }
 for v in "$@"; do
@@ -29,6 +29,8 @@ for v in "$@"; do
         xcd) variant xcd -DTRT_XCD_SWIZZLE ;;
         libmpow) variant libmpow -DTRT_LIBM_POW ;;
         trivial) variant trivial -DTRT_DIAG_TRIVIAL ;;
+        noenvfetch) variant noenvfetch -DTRT_DIAG_NO_ENV_FETCH ;;
+        clock) variant clock -DTRT_DIAG_WAVE_CLOCK ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac
 done

@@ -3,7 +3,7 @@ nobodyscool/vkComputeShader_tinyraytracer (shader.comp cast_ray) as a hand-writt
 kernel behind a C-ABI (include/trt/abi.h)."""
 from . import types
 from ._lib import ABI_SYMBOLS, LIB_PATH, TrtError, lib
-from .renderer import Renderer, render
+from .renderer import Renderer, render, write_image
 from .scene import (
     CONFIGS,
     MODEL_INFOS,
@@ -23,5 +23,5 @@ from .scene import (
 __all__ = [
     "types", "ABI_SYMBOLS", "LIB_PATH", "TrtError", "lib", "Renderer", "render", "CONFIGS",
     "MODEL_INFOS", "Scene", "SceneBuilder", "config_c1", "config_c2", "config_c3", "config_c4",
-    "config_c5", "config_reference_default", "icosphere", "make_ubo", "synthetic_envmap",
+    "config_c5", "config_reference_default", "icosphere", "make_ubo", "synthetic_envmap", "write_image",
 ]

@@ -62,6 +62,8 @@ def lib() -> ctypes.CDLL:
         "trt_scene_model_count": (c_u32, [vp]),
         "trt_scene_triangles": (vp, [vp]),
         "trt_scene_models": (vp, [vp]),
+        "trt_write_ppm": (c_int, [ctypes.c_char_p, vp, c_u32, c_u32]),
+        "trt_write_png": (c_int, [ctypes.c_char_p, vp, c_u32, c_u32]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -96,4 +98,6 @@ ABI_SYMBOLS = (
     "trt_scene_model_count",
     "trt_scene_triangles",
     "trt_scene_models",
+    "trt_write_ppm",
+    "trt_write_png",
 )

@@ -71,6 +71,13 @@ __device__ __forceinline__ float pow_pos(float x, float y) {
 #endif
 __device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
+// Linear -> sRGB transfer (IEC 61966-2-1) the presentation engine applies when shader.frag
+// writes the sampled RGBA32F image (main.cpp:869) to the B8G8R8A8_SRGB swapchain
+// (main.cpp:2341).  x in [0, 1].
+__device__ __forceinline__ float srgb_encode(float x) {
+    return x <= 0.0031308f ? 12.92f * x : 1.055f * pow_pos(x, 1.0f / 2.4f) - 0.055f;
+}
+
 // ---- primitives (shader.comp line refs) -------------------------------------------------
 
 // ray_aabb_intersect, shader.comp:197-207
@@ -425,6 +432,12 @@ __device__ __forceinline__ float unorm8(uint32_t c) { return (float)c / 255.0f; 
 
 __device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
     if (!(A.flags & TRT_FLAG_ENVMAP)) return mk(0.2f, 0.7f, 0.8f); // BACKGROUND_COLOR :77
+#ifdef TRT_DIAG_NO_ENV_FETCH
+    {   // diagnostic: uv math without the texel gathers
+        float u = (atan2f(d.z, d.x) + TRT_PI) / (2.0f * TRT_PI), v = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f)) / TRT_PI;
+        return mk(u, v, u * v);
+    }
+#endif
     float theta = atan2f(d.z, d.x);
     float phi = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
     float u = (theta + TRT_PI) / (2.0f * TRT_PI);
@@ -725,9 +738,15 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
         reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
     }
     if (A.out8) { // rgba8 storage image, shader.comp:61, 600
-        uint32_t r = (uint32_t)floorf(gx * 255.0f + 0.5f);
-        uint32_t g = (uint32_t)floorf(gy * 255.0f + 0.5f);
-        uint32_t b = (uint32_t)floorf(gz * 255.0f + 0.5f);
+        float ex = gx, ey = gy, ez = gz;
+        if (A.flags & TRT_FLAG_SRGB_OUT) { // as displayed through the sRGB swapchain
+            ex = srgb_encode(gx);
+            ey = srgb_encode(gy);
+            ez = srgb_encode(gz);
+        }
+        uint32_t r = (uint32_t)floorf(ex * 255.0f + 0.5f);
+        uint32_t g = (uint32_t)floorf(ey * 255.0f + 0.5f);
+        uint32_t b = (uint32_t)floorf(ez * 255.0f + 0.5f);
         A.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
     }
 }
@@ -771,7 +790,24 @@ __global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
     __shared__ float4 slab[GEOM == 1 ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
     Cnt cnt;
+#ifdef TRT_DIAG_WAVE_CLOCK
+    // diagnostic: per-workgroup (tile, start, end) of the 100 MHz constant clock into out32
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
+#ifdef TRT_DIAG_WAVE_CLOCK
+    __syncthreads();
+    if (threadIdx.x == 0 && A.out32) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t* rec = reinterpret_cast<uint32_t*>(A.out32) + 4 * (size_t)blockIdx.x;
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        rec[0] = xcd_tile(A, blockIdx.x) | ((xcc & 15u) << 28);
+        rec[1] = (uint32_t)t_start;
+        rec[2] = (uint32_t)t_end;
+        rec[3] = (uint32_t)(t_start >> 32);
+    }
+#endif
     if (COUNT) {
         const uint32_t v[10] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt};
 #pragma unroll

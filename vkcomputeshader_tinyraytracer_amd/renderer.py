@@ -10,6 +10,7 @@ tensors (device, rendered in place on the context's stream).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -170,3 +171,21 @@ def render(scene: Scene, device: int = 0, **kw):
     with Renderer(device) as r:
         r.upload_scene(scene)
         return r.draw_frame(scene.params(), **kw)
+
+
+def write_image(path, rgba8) -> None:
+    """Writes an (H, W, 4) uint8 frame (numpy, or a torch tensor) as .png or .ppm through the
+    C-ABI writers (trt_write_png / trt_write_ppm)."""
+    if hasattr(rgba8, "detach"):
+        rgba8 = rgba8.detach().cpu().numpy()
+    a = np.ascontiguousarray(rgba8, np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError(f"expected (H, W, 4) RGBA8, got {a.shape}")
+    path = os.fspath(path)
+    ext = os.path.splitext(path)[1].lower()
+    fn = {".png": "trt_write_png", ".ppm": "trt_write_ppm"}.get(ext)
+    if fn is None:
+        raise ValueError(f"unsupported image extension {ext!r} (.png or .ppm)")
+    rc = getattr(lib(), fn)(path.encode(), a.ctypes.data, a.shape[1], a.shape[0])
+    if rc != 0:
+        raise TrtError(rc, f"{fn}({path!r}) failed")

@@ -58,6 +58,7 @@ FLAG_DEVICE_PTRS = 1 << 5
 FLAG_COUNT = 1 << 6
 FLAG_TIMING = 1 << 7
 FLAG_BATCH_WALK = 1 << 8
+FLAG_SRGB_OUT = 1 << 9
 FLAGS_REFERENCE = FLAG_FLOOR | FLAG_ENVMAP | FLAG_ROW_QUIRK
 
 MAX_DEPTH_LIMIT = 20
