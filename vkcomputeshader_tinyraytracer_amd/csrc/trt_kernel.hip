@@ -734,7 +734,12 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     // pow(color, vec3(GAMMA)), shader.comp:598
     const float gx = pow_pos(acc.x, TRT_GAMMA), gy = pow_pos(acc.y, TRT_GAMMA), gz = pow_pos(acc.z, TRT_GAMMA);
     const size_t o = (size_t)k * A.width + x;
-    if (A.out32) { // rayOut[idx].resultColor, shader.comp:601
+#ifdef TRT_DIAG_WAVE_CLOCK
+    if (false) // out32 carries the workgroup clock records
+#else
+    if (A.out32) // rayOut[idx].resultColor, shader.comp:601
+#endif
+    {
         reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
     }
     if (A.out8) { // rgba8 storage image, shader.comp:61, 600
@@ -791,7 +796,8 @@ __global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
     __shared__ float4 slab[GEOM == 1 ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
     Cnt cnt;
 #ifdef TRT_DIAG_WAVE_CLOCK
-    // diagnostic: per-workgroup (tile, start, end) of the 100 MHz constant clock into out32
+    // diagnostic: per-workgroup (tile | xcc << 28, start lo, duration, start hi) of the
+    // 100 MHz constant clock, written to out32 (tools/waveclock.py)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
@@ -804,7 +810,7 @@ __global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         rec[0] = xcd_tile(A, blockIdx.x) | ((xcc & 15u) << 28);
         rec[1] = (uint32_t)t_start;
-        rec[2] = (uint32_t)t_end;
+        rec[2] = (uint32_t)(t_end - t_start);
         rec[3] = (uint32_t)(t_start >> 32);
     }
 #endif
