@@ -186,6 +186,56 @@ uint32_t trt_scene_model_count(const trt_scene* s);
 const trt_triangle* trt_scene_triangles(const trt_scene* s);
 const trt_model* trt_scene_models(const trt_scene* s);
 
+/* ---- envmap JPEG ---------------------------------------------------------
+ * The reference reads its envmap with stb_image v2.22, stbi_load(path, ..., STBI_rgb_alpha)
+ * (main.cpp:928-949), then uploads it as binding 4.  This path decodes the same files to the
+ * same RGBA8 bytes: the entropy decode (Huffman, baseline and progressive scans) runs on the
+ * host into coefficient planes (trt_jpeg_*), and dequantisation, IDCT, chroma upsampling and
+ * colour conversion run on the GPU (trt_jpeg_decode), straight into device memory. */
+
+/* colour model of the RGBA output (stb's load_jpeg_image) */
+#define TRT_JPEG_GRAY 0
+#define TRT_JPEG_YCBCR 1
+#define TRT_JPEG_RGB 2  /* component ids 'R','G','B', or Adobe transform 0 without JFIF */
+#define TRT_JPEG_CMYK 3 /* 4 components, Adobe transform 0 */
+#define TRT_JPEG_YCCK 4 /* 4 components, Adobe transform 2 */
+
+typedef struct trt_jpeg trt_jpeg;
+
+typedef struct trt_jpeg_info {
+    uint32_t width, height;
+    uint32_t components;  /* 1, 3 or 4 */
+    uint32_t progressive; /* SOF2 */
+    int32_t color;        /* TRT_JPEG_* */
+    uint32_t hmax, vmax;  /* largest sampling factors */
+    uint32_t h[4], v[4];  /* per-component sampling factors */
+    uint32_t blocks_w[4], blocks_h[4]; /* MCU-padded block grid of each coefficient plane */
+} trt_jpeg_info;
+
+int trt_jpeg_create(trt_jpeg** out);
+void trt_jpeg_destroy(trt_jpeg* j);
+const char* trt_jpeg_last_error(const trt_jpeg* j);
+
+/* Parses `len` bytes of a JPEG file and entropy-decodes every scan (host). */
+int trt_jpeg_parse(trt_jpeg* j, const uint8_t* data, size_t len);
+int trt_jpeg_get_info(const trt_jpeg* j, trt_jpeg_info* info);
+
+/* Raw (not dequantised) coefficients of component c: blocks_w * blocks_h blocks of 64
+ * int16 in natural (row-major) order; and its 64-entry quantisation table.  NULL if c is
+ * out of range or nothing was parsed. */
+const int16_t* trt_jpeg_coefficients(const trt_jpeg* j, uint32_t c);
+const uint16_t* trt_jpeg_quant(const trt_jpeg* j, uint32_t c);
+
+/* GPU reconstruction of a parsed JPEG into width * height * 4 bytes of RGBA8 (alpha 255), the
+ * buffer stbi_load(..., STBI_rgb_alpha) returns.  Host pointer unless TRT_FLAG_DEVICE_PTRS.
+ * Synchronous. */
+int trt_jpeg_decode(trt_ctx* ctx, const trt_jpeg* j, uint8_t* out_rgba8, uint32_t flags);
+
+/* Binding 4 from JPEG bytes (the reference's stbi_load + texture upload, main.cpp:928-1111):
+ * replaces the context's envmap.  Call after trt_upload_scene (which replaces every
+ * binding). */
+int trt_upload_envmap_jpeg(trt_ctx* ctx, const uint8_t* data, size_t len);
+
 /* ---- frame files (the reference only presents, main.cpp:2181-2205) ------- */
 
 /* Binary PPM (P6, RGB; alpha dropped) of a host RGBA8 frame, e.g. trt_render's out_rgba8. */

@@ -62,6 +62,15 @@ def lib() -> ctypes.CDLL:
         "trt_scene_model_count": (c_u32, [vp]),
         "trt_scene_triangles": (vp, [vp]),
         "trt_scene_models": (vp, [vp]),
+        "trt_jpeg_create": (c_int, [ctypes.POINTER(vp)]),
+        "trt_jpeg_destroy": (None, [vp]),
+        "trt_jpeg_last_error": (ctypes.c_char_p, [vp]),
+        "trt_jpeg_parse": (c_int, [vp, vp, ctypes.c_size_t]),
+        "trt_jpeg_get_info": (c_int, [vp, vp]),
+        "trt_jpeg_coefficients": (vp, [vp, c_u32]),
+        "trt_jpeg_quant": (vp, [vp, c_u32]),
+        "trt_jpeg_decode": (c_int, [vp, vp, vp, c_u32]),
+        "trt_upload_envmap_jpeg": (c_int, [vp, vp, ctypes.c_size_t]),
         "trt_write_ppm": (c_int, [ctypes.c_char_p, vp, c_u32, c_u32]),
         "trt_write_png": (c_int, [ctypes.c_char_p, vp, c_u32, c_u32]),
     }
@@ -98,6 +107,15 @@ ABI_SYMBOLS = (
     "trt_scene_model_count",
     "trt_scene_triangles",
     "trt_scene_models",
+    "trt_jpeg_create",
+    "trt_jpeg_destroy",
+    "trt_jpeg_last_error",
+    "trt_jpeg_parse",
+    "trt_jpeg_get_info",
+    "trt_jpeg_coefficients",
+    "trt_jpeg_quant",
+    "trt_jpeg_decode",
+    "trt_upload_envmap_jpeg",
     "trt_write_ppm",
     "trt_write_png",
 )

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/trt/abi.h"
+#include "jpeg.h"
 #include "trt_device.h"
 
 namespace trt {
@@ -600,3 +601,61 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
 }
 
 } // extern "C"
+
+// ---- envmap JPEG: host entropy decode + GPU reconstruction ----------------
+
+namespace trt {
+namespace jpeg {
+const Image* image_of(const trt_jpeg* j);
+}
+} // namespace trt
+
+extern "C" int trt_jpeg_decode(trt_ctx* c, const trt_jpeg* j, uint8_t* out, uint32_t flags) {
+    if (!c) return TRT_ERR_INVALID;
+    const trt::jpeg::Image* im = trt::jpeg::image_of(j);
+    if (!im) return fail(c, TRT_ERR_INVALID, "trt_jpeg_decode: nothing parsed");
+    if (!out) return fail(c, TRT_ERR_INVALID, "trt_jpeg_decode: null output");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t bytes = (size_t)im->width * im->height * 4;
+    uint8_t* dst = out;
+    if (!(flags & TRT_FLAG_DEVICE_PTRS)) {
+        int rc = ensure(c, &c->d_out8, &c->cap8, bytes, "jpeg output");
+        if (rc != TRT_OK) return rc;
+        dst = static_cast<uint8_t*>(c->d_out8);
+    }
+    HIP_TRY(c, trt::jpeg::reconstruct(*im, dst, c->stream));
+    if (!(flags & TRT_FLAG_DEVICE_PTRS)) {
+        HIP_TRY(c, hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    return TRT_OK;
+}
+
+extern "C" int trt_upload_envmap_jpeg(trt_ctx* c, const uint8_t* data, size_t len) {
+    if (!c) return TRT_ERR_INVALID;
+    trt_jpeg* j = nullptr;
+    int rc = trt_jpeg_create(&j);
+    if (rc != TRT_OK) return fail(c, rc, "trt_upload_envmap_jpeg: out of memory");
+    rc = trt_jpeg_parse(j, data, len);
+    if (rc != TRT_OK) {
+        std::string msg = std::string("trt_upload_envmap_jpeg: ") + trt_jpeg_last_error(j);
+        trt_jpeg_destroy(j);
+        return fail(c, rc, msg);
+    }
+    const trt::jpeg::Image* im = trt::jpeg::image_of(j);
+    hipError_t e = hipSetDevice(c->device);
+    uint32_t* d = nullptr;
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), (size_t)im->width * im->height * 4);
+    if (e == hipSuccess) e = trt::jpeg::reconstruct(*im, reinterpret_cast<uint8_t*>(d), c->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        trt_jpeg_destroy(j);
+        return hip_fail(c, e, "trt_upload_envmap_jpeg");
+    }
+    (void)hipFree(c->d_env);
+    c->d_env = d;
+    c->env_w = (uint32_t)im->width;
+    c->env_h = (uint32_t)im->height;
+    trt_jpeg_destroy(j);
+    return TRT_OK;
+}

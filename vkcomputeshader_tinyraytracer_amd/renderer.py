@@ -148,6 +148,31 @@ class Renderer:
         self._check(self._L.trt_frame_times(self._h, ms, n))
         return np.frombuffer(ms, np.float32).copy()
 
+    # -- envmap JPEG -----------------------------------------------------------
+    def decode_jpeg(self, jpeg, out=None):
+        """stbi_load(..., STBI_rgb_alpha) of a JPEG (bytes, path or JpegFile): host entropy
+        decode + GPU reconstruction.  Returns an (H, W, 4) uint8 numpy array, or renders into
+        `out` when it is a torch CUDA tensor."""
+        from .jpeg import JpegFile
+
+        jf = jpeg if isinstance(jpeg, JpegFile) else JpegFile(jpeg)
+        h, w = jf.shape
+        if _is_torch_cuda(out):
+            assert out.is_contiguous() and out.numel() >= h * w * 4
+            self._check(self._L.trt_jpeg_decode(self._h, jf.handle, out.data_ptr(), T.FLAG_DEVICE_PTRS))
+            return out
+        img = np.empty((h, w, 4), np.uint8)
+        self._check(self._L.trt_jpeg_decode(self._h, jf.handle, img.ctypes.data, 0))
+        return img
+
+    def upload_envmap_jpeg(self, data) -> None:
+        """Binding 4 from JPEG bytes or a path (after upload_scene)."""
+        if isinstance(data, (str, os.PathLike)):
+            with open(data, "rb") as f:
+                data = f.read()
+        buf = bytes(data)
+        self._check(self._L.trt_upload_envmap_jpeg(self._h, buf, len(buf)))
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._L.trt_destroy(self._h)
