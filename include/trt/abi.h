@@ -128,15 +128,29 @@ int trt_update_ubo(trt_ctx* ctx, const trt_ubo* ubo);
 int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out_rgba32f,
                trt_stats* st);
 
+/* Frames in flight of trt_render_frames (the reference's MAX_FRAMES_IN_FLIGHT = 2,
+ * main.cpp:45: per-frame command buffers, UBOs and rayOut buffers, main.cpp:1518-1664, with
+ * no barrier between consecutive compute submissions).  Frame i of a trt_render_frames call
+ * runs on in-flight slot i % n: slot 0 is the context's stream, slots 1..n-1 are streams the
+ * context owns, forked from and joined back into its stream inside the call, so frame i+1's
+ * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 4]; default 2. */
+#define TRT_FRAMES_IN_FLIGHT_DEFAULT 2u
+#define TRT_MAX_FRAMES_IN_FLIGHT 4u
+int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
+
 /* The reference's frame loop (mainLoop -> drawFrame, main.cpp:405-438, 2181-2205) in one
  * call: for each of `nframes` frames, updateUniformBuffer with ubos[i] (or the current UBO
  * when ubos is NULL) and enqueue one trace launch writing out_rgba8 + i * frame_stride
- * bytes (frame_stride 0 = every frame overwrites the same image).  Requires
- * TRT_FLAG_DEVICE_PTRS; only enqueues.  Host cost per frame is one kernel launch, so
- * back-to-back frames keep the GPU busy.  With TRT_FLAG_TIMING a HIP event pair brackets
- * the launch of every `time_every`-th frame (0 or 1: every frame) on the stream — an event
- * pair costs a few microseconds of queue time, so a sparse sample keeps a timed frame loop
- * representative; trt_frame_times() reads the sampled kernel times. */
+ * bytes.  Frames in flight (above) may run concurrently: give concurrent frames distinct
+ * images (frame_stride >= rows*width*4) unless they are identical — frame_stride 0 makes
+ * every frame write the same image, like the reference's single storage image (binding 3,
+ * main.cpp:865-926).  Requires TRT_FLAG_DEVICE_PTRS; only enqueues; all frames have
+ * completed on the context's stream when work enqueued after the call runs.  Host cost per
+ * frame is one kernel launch.  With TRT_FLAG_TIMING a HIP event pair brackets the launch of
+ * every `time_every`-th frame (0 or 1: every frame) on its slot's stream (the span includes
+ * any overlap with the other slots' frames) — an event pair costs a few microseconds of
+ * queue time, so a sparse sample keeps a timed frame loop representative;
+ * trt_frame_times() reads the sampled kernel times. */
 int trt_render_frames(trt_ctx* ctx, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
                       uint8_t* out_rgba8, size_t frame_stride, uint32_t time_every);
 

@@ -241,6 +241,42 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
         assert np.array_equal(out[i].cpu().numpy(), one)
 
 
+@pytest.mark.parametrize("inflight", [1, 2, 3, 4])
+def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
+    """Frames in flight (trt_set_frames_in_flight, main.cpp:45): concurrent frames with
+    distinct UBOs and images equal one-at-a-time trt_render, and all of them have landed on
+    the caller's stream when render_frames returns (no explicit join by the caller)."""
+    torch = pytest.importorskip("torch")
+    sc = S.config_c2(96, 64, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    n = 9
+    ubos = np.stack([S.make_ubo(cam=(0.07 * i, 0.02 * i, -0.1 * i)) for i in range(n)])
+    out = torch.zeros((n, 64, 96, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    gpu_renderer.set_stream(stream)
+    try:
+        gpu_renderer.set_frames_in_flight(inflight)
+        gpu_renderer.render_frames(sc.params(), out, n, ubos=ubos, frame_stride=64 * 96 * 4)
+        # work enqueued on the caller's stream after the call sees every frame
+        with torch.cuda.stream(stream):
+            snap = out.clone()
+        stream.synchronize()
+    finally:
+        gpu_renderer.set_frames_in_flight(2)
+        gpu_renderer.set_stream(None)
+    for i in range(n):
+        gpu_renderer.update_ubo(ubos[i])
+        one, _, _ = gpu_renderer.draw_frame(sc.params())
+        assert np.array_equal(snap[i].cpu().numpy(), one), i
+
+
+def test_frames_in_flight_bounds(gpu_renderer):
+    for bad in (0, 5):
+        with pytest.raises(TrtError):
+            gpu_renderer.set_frames_in_flight(bad)
+    gpu_renderer.set_frames_in_flight(2)
+
+
 def test_duplicate_triangles_first_batch_wins(gpu_renderer):
     """Two copies of one mesh at the same place with different materials: every hit is a t
     tie, and the reference's strict `t < nearest` (shader.comp:349) keeps the copy in the

@@ -6,7 +6,7 @@ for round in 1 2; do
   for cfg in ${CONFIGS:-C2}; do
     timeout -k 10 200 python tools/kbench.py --config $cfg --frames ${FRAMES:-200} --tag product || exit $?
     for v in ${VARIANTS:-base}; do
-      TRT_LIB=diag/libtrt_$v.so timeout -k 10 200 python tools/kbench.py --config $cfg --frames ${FRAMES:-200} --tag $v || exit $?
+      TRT_LIB=variants/libtrt_$v.so timeout -k 10 200 python tools/kbench.py --config $cfg --frames ${FRAMES:-200} --tag $v || exit $?
     done
   done
 done

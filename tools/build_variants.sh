@@ -1,23 +1,25 @@
 #!/usr/bin/env bash
-# Experimental builds of libtrt.so for A/B timing (loaded with TRT_LIB=diag/libtrt_<name>.so).
+# Experimental builds of libtrt.so for A/B timing (loaded with TRT_LIB=variants/libtrt_<name>.so).
 # Diagnostic variants change results (they price one stage) and are never the product.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/vkcomputeshader_tinyraytracer_amd/csrc
-OUT=$ROOT/diag
+OUT=$ROOT/variants
 mkdir -p "$OUT" "$ROOT/build/diag"
 FP="-ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math -fno-slp-vectorize"
 HOST="-O2 -std=c++17 -fPIC -ffp-contract=off -I/opt/rocm/include -D__HIP_PLATFORM_AMD__"
-for f in trt_runtime scene_build obj_load bvh_build image_io; do
+for f in trt_runtime scene_build obj_load bvh_build image_io jpeg_entropy jpeg_api; do
     [ "$ROOT/build/diag/$f.o" -nt "$SRC/$f.cpp" ] || /opt/rocm/bin/hipcc $HOST -x c++ -c -o "$ROOT/build/diag/$f.o" "$SRC/$f.cpp"
 done
 variant() { # name extra-flags...
     local name=$1
     shift
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "$@" -c -o "$ROOT/build/diag/k_$name.o" "$SRC/trt_kernel.hip"
+    [ "$ROOT/build/diag/jpeg_kernel.o" -nt "$SRC/jpeg_kernel.hip" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -c -o "$ROOT/build/diag/jpeg_kernel.o" "$SRC/jpeg_kernel.hip"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libtrt_$name.so" "$ROOT/build/diag/k_$name.o" \
         "$ROOT/build/diag/trt_runtime.o" "$ROOT/build/diag/scene_build.o" "$ROOT/build/diag/obj_load.o" \
-        "$ROOT/build/diag/bvh_build.o" "$ROOT/build/diag/image_io.o" -lz
+        "$ROOT/build/diag/bvh_build.o" "$ROOT/build/diag/image_io.o" "$ROOT/build/diag/jpeg_entropy.o" \
+        "$ROOT/build/diag/jpeg_api.o" "$ROOT/build/diag/jpeg_kernel.o" -lz
     echo "built $OUT/libtrt_$name.so"
 }
 for v in "$@"; do
@@ -31,6 +33,10 @@ for v in "$@"; do
         trivial) variant trivial -DTRT_DIAG_TRIVIAL ;;
         noenvfetch) variant noenvfetch -DTRT_DIAG_NO_ENV_FETCH ;;
         clock) variant clock -DTRT_DIAG_WAVE_CLOCK ;;
+        prio1) variant prio1 -DTRT_PRIO=1 ;;
+        prio3) variant prio3 -DTRT_PRIO=3 ;;
+        w5) variant w5 -DTRT_WAVES=5 ;;
+        w5prio) variant w5prio -DTRT_WAVES=5 -DTRT_PRIO=3 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac
 done

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Workgroup timeline of one frame (diagnostic build: TRT_LIB=diag/libtrt_clock.so, built by
+"""Workgroup timeline of one frame (diagnostic build: TRT_LIB=variants/libtrt_clock.so, built by
 tools/build_variants.sh clock).  Each 64-lane workgroup (one 8x8 tile) records its tile, XCD
 and start/end of the 100 MHz constant clock; this prints the frame span, workgroup duration
 percentiles, the occupancy curve and the tail (time the last workgroups run alone).
 
-  TRT_LIB=diag/libtrt_clock.so python tools/waveclock.py [--config C2] [--out f.npz]
+  TRT_LIB=variants/libtrt_clock.so python tools/waveclock.py [--config C2] [--out f.npz]
 """
 from __future__ import annotations
 

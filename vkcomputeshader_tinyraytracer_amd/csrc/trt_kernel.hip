@@ -428,7 +428,15 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
 
 // ---- background (direction_to_uv + texture(), shader.comp:410-416, 455-458) --------------
 
-__device__ __forceinline__ float unorm8(uint32_t c) { return (float)c / 255.0f; }
+// UNORM8 -> float, c / 255 correctly rounded (the oracle's `(float)c / 255.0f`), as
+// q = c * RN(1/255) plus one FMA remainder correction: bit-identical to the IEEE quotient for
+// every c in [0, 255] (exhaustive exact-rational check: tests/test_envmap_math.py), 3 VALU ops
+// instead of the 11-instruction correctly-rounded division sequence (12 per envmap sample).
+__device__ __forceinline__ float unorm8(uint32_t c) {
+    const float x = (float)c, r = 1.0f / 255.0f;
+    const float q = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
+}
 
 __device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
     if (!(A.flags & TRT_FLAG_ENVMAP)) return mk(0.2f, 0.7f, 0.8f); // BACKGROUND_COLOR :77
@@ -440,8 +448,11 @@ __device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
 #endif
     float theta = atan2f(d.z, d.x);
     float phi = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
-    float u = (theta + TRT_PI) / (2.0f * TRT_PI);
-    float v = phi / TRT_PI;
+    // direction_to_uv, shader.comp:410-416.  atan/acos are already ocml's (within a few ulp
+    // of the oracle's libm, tests/helpers.py FLOAT_TOL), so the two divisions by constants
+    // are products with the rounded reciprocals (<= 1 ulp apart from the quotients).
+    float u = (theta + TRT_PI) * (1.0f / (2.0f * TRT_PI));
+    float v = phi * (1.0f / TRT_PI);
     // Sampler: LINEAR, CLAMP_TO_EDGE, level 0 (main.cpp:1091-1106), R8G8B8A8_UNORM.
     const int W = (int)A.env_w, H = (int)A.env_h;
     float x = u * (float)W - 0.5f, y = v * (float)H - 0.5f;
@@ -534,6 +545,9 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
     Seg cur{orig, dir, 1.0f, 0};
     for (;;) {
         if (COUNT && cur.depth > 0) ++cnt.sec;
+#ifdef TRT_PRIO
+        if (cur.depth > 0) __builtin_amdgcn_s_setprio(TRT_PRIO);
+#endif
         Hit h;
         scene_intersect<COUNT, GEOM>(A, cur.o, cur.d, h, cnt, slab);
         bool have_next = false;
@@ -790,8 +804,11 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
 // static grid-stride over the resident waves 1.2-2x slower from imbalance.)
 // GEOM: 0 = no triangles (spheres/floor only, e.g. C1/C2: the triangle code is compiled
 // out, 4 waves per SIMD); 1 = the reference-order batch walk; 2 = per-lane BVH.
+#ifndef TRT_WAVES
+#define TRT_WAVES 1
+#endif
 template <int CAP, bool COUNT, int GEOM>
-__global__ __launch_bounds__(64) void trace_kernel(KArgs A) {
+__global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
     __shared__ float4 slab[GEOM == 1 ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
     Cnt cnt;

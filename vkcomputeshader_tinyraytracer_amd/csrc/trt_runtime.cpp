@@ -64,6 +64,10 @@ struct trt_ctx {
     uint32_t num_cus = 256;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
+    uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
+    std::vector<hipStream_t> aux; // frames-in-flight streams (frame i -> stream i % n)
+    std::vector<hipEvent_t> aux_ev;
+    hipEvent_t fork_ev = nullptr;
     uint32_t fev_frames = 0;
 };
 
@@ -220,6 +224,12 @@ int trt_destroy(trt_ctx* c) {
     (void)hipFree(c->d_rays);
     (void)hipFree(c->d_counters);
     for (hipEvent_t e : c->fev) (void)hipEventDestroy(e);
+    for (hipStream_t s : c->aux) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+    }
+    for (hipEvent_t e : c->aux_ev) (void)hipEventDestroy(e);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -232,6 +242,14 @@ const char* trt_last_error(const trt_ctx* c) { return c ? c->err.c_str() : "null
 int trt_set_stream(trt_ctx* c, void* s) {
     if (!c) return TRT_ERR_INVALID;
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+    return TRT_OK;
+}
+
+int trt_set_frames_in_flight(trt_ctx* c, uint32_t n) {
+    if (!c) return TRT_ERR_INVALID;
+    if (n < 1 || n > TRT_MAX_FRAMES_IN_FLIGHT)
+        return fail(c, TRT_ERR_INVALID, "trt_set_frames_in_flight: n must be in [1, TRT_MAX_FRAMES_IN_FLIGHT]");
+    c->frames_in_flight = n;
     return TRT_OK;
 }
 
@@ -495,20 +513,46 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
     fill_args(c, p, A);
     A.rays_in = reinterpret_cast<const float*>(p->rays_in);
     if (A.rows == 0) return TRT_OK;
+    // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): frame i runs on slot i % n.  Slot 0
+    // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
+    // joined back into it below, so to the caller all frames complete on its stream.
+    const uint32_t nfl = std::min(c->frames_in_flight, std::max(nframes, 1u));
+    std::vector<hipStream_t> sv{c->stream};
+    if (nfl > 1) {
+        while (c->aux.size() < nfl - 1) {
+            hipStream_t s;
+            HIP_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            c->aux.push_back(s);
+            hipEvent_t e;
+            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->aux_ev.push_back(e);
+        }
+        if (!c->fork_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->fork_ev, c->stream));
+        for (uint32_t k = 0; k + 1 < nfl; ++k) {
+            HIP_TRY(c, hipStreamWaitEvent(c->aux[k], c->fork_ev, 0));
+            sv.push_back(c->aux[k]);
+        }
+    }
     for (uint32_t i = 0; i < nframes; ++i) {
         if (ubos) {
             c->ubo = ubos[i];
             fill_ubo_args(A, c->ubo);
         }
+        hipStream_t st = sv[i % nfl];
         A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
         const bool timed = timing && i % every == 0;
         const size_t k = 2 * (size_t)(i / every);
-        if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], c->stream));
-        HIP_TRY(c, trt::launch_trace(A, c->stream, false));
+        if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], st));
+        HIP_TRY(c, trt::launch_trace(A, st, false));
         if (timed) {
-            HIP_TRY(c, hipEventRecord(c->fev[k + 1], c->stream));
+            HIP_TRY(c, hipEventRecord(c->fev[k + 1], st));
             c->fev_frames = i / every + 1;
         }
+    }
+    for (uint32_t k = 0; k + 1 < nfl; ++k) {
+        HIP_TRY(c, hipEventRecord(c->aux_ev[k], c->aux[k]));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->aux_ev[k], 0));
     }
     return TRT_OK;
 }

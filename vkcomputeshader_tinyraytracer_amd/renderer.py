@@ -56,6 +56,11 @@ class Renderer:
         u = np.ascontiguousarray(ubo)
         self._check(self._L.trt_update_ubo(self._h, u.ctypes.data))
 
+    def set_frames_in_flight(self, n: int) -> None:
+        """Frames of render_frames that may run concurrently (trt_set_frames_in_flight; the
+        reference's MAX_FRAMES_IN_FLIGHT = 2, main.cpp:45)."""
+        self._check(self._L.trt_set_frames_in_flight(self._h, int(n)))
+
     def set_stream(self, stream) -> None:
         """`stream`: a torch.cuda.Stream (not the legacy default stream), a raw hipStream_t
         int, or None (the context's own stream)."""
