@@ -14,7 +14,7 @@ done
 variant() { # name extra-flags...
     local name=$1
     shift
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "$@" -c -o "$ROOT/build/diag/k_$name.o" "$SRC/trt_kernel.hip"
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "$@" -c -o "$ROOT/build/diag/k_$name.o" "${KSRC:-$SRC/trt_kernel.hip}"
     [ "$ROOT/build/diag/jpeg_kernel.o" -nt "$SRC/jpeg_kernel.hip" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -c -o "$ROOT/build/diag/jpeg_kernel.o" "$SRC/jpeg_kernel.hip"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libtrt_$name.so" "$ROOT/build/diag/k_$name.o" \
         "$ROOT/build/diag/trt_runtime.o" "$ROOT/build/diag/scene_build.o" "$ROOT/build/diag/obj_load.o" \
@@ -36,6 +36,13 @@ for v in "$@"; do
         prio1) variant prio1 -DTRT_PRIO=1 ;;
         prio3) variant prio3 -DTRT_PRIO=3 ;;
         w5) variant w5 -DTRT_WAVES=5 ;;
+        tpw2) variant tpw2 -DTRT_TPW=2 ;;
+        fmexec) variant fmexec -DTRT_FM_EXEC_BRANCH ;;
+        prev) # the kernel of git revision $PREV (default HEAD), for A/B against the work tree
+            git -C "$ROOT" show "${PREV:-HEAD}:vkcomputeshader_tinyraytracer_amd/csrc/trt_kernel.hip" > "$SRC/.prev_kernel.hip"
+            KSRC="$SRC/.prev_kernel.hip" variant prev
+            rm -f "$SRC/.prev_kernel.hip" ;;
+        tpw4) variant tpw4 -DTRT_TPW=4 ;;
         w5prio) variant w5prio -DTRT_WAVES=5 -DTRT_PRIO=3 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac

@@ -35,7 +35,7 @@ def main():
     kw = {}
     if a.width:
         kw = dict(width=a.width, height=a.height)
-    if a.config == "ref":
+    if a.config == "ref":  # the shipped glass+water+ice frame
         sc = S.config_reference_default(**kw)
     else:
         sc = S.CONFIGS[a.config](**kw)

@@ -25,6 +25,7 @@
 
 #include "../../include/trt/abi.h"
 #include "trt_device.h"
+#include "trt_math.h"
 
 namespace trt {
 
@@ -45,11 +46,12 @@ __device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
     return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
+// normalize / length with the contract's correctly rounded 1 / sqrt(.) (trt_math.h).
 __device__ __forceinline__ f3 normalize3(f3 v) {
-    float inv = 1.0f / sqrtf(dot3(v, v));
+    float inv = rsqrt_rn2(dot3(v, v));
     return muls(v, inv);
 }
-__device__ __forceinline__ float length3(f3 v) { return sqrtf(dot3(v, v)); }
+__device__ __forceinline__ float length3(f3 v) { return sqrt_rn(dot3(v, v)); }
 // GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
 __device__ __forceinline__ f3 reflect3(f3 I, f3 N) {
     float k = 2.0f * dot3(N, I);
@@ -96,7 +98,7 @@ __device__ __forceinline__ bool sphere_hit(f3 o, f3 d, const SphereArg& s, float
     float d2 = dot3(L, L) - tca * tca;
     float r2 = s.r * s.r;
     if (d2 > r2) return false;
-    float thc = sqrtf(r2 - d2);
+    float thc = sqrt_rn(r2 - d2);
     float t0 = tca - thc, t1 = tca + thc;
     if (t0 > TRT_EPS) t = t0;
     else if (t1 > TRT_EPS) t = t1;
@@ -109,10 +111,10 @@ __device__ __forceinline__ f3 custom_refract(f3 I, f3 N, float eta_out, float et
     bool entering = dot3(I, N) < 0.0f;
     f3 fn = entering ? N : neg(N);
     float cosi = clamp01(dot3(neg(I), fn));
-    float eta = entering ? eta_in / eta_out : eta_out / eta_in;
+    float eta = entering ? div_rn(eta_in, eta_out) : div_rn(eta_out, eta_in);
     float sint2 = eta * eta * (1.0f - cosi * cosi);
     if (sint2 > 1.0f) return mk(0.0f, 0.0f, 0.0f);
-    float k = sqrtf(1.0f - sint2);
+    float k = sqrt_rn(1.0f - sint2);
     f3 r = add(muls(I, eta), muls(fn, eta * cosi - k));
     return normalize3(r);
 }
@@ -225,7 +227,7 @@ __device__ __forceinline__ void walk_batches(const KArgs& A, f3 o, f3 d, f3 inv,
                         f3 hv = cross3(d, e2);
                         float a = dot3(e1, hv);
                         if (a > -TRT_EPS && a < TRT_EPS) continue;
-                        float f = 1.0f / a;
+                        float f = rcp_rn_lane(a);
                         f3 sv = sub(o, v0);
                         float u = f * dot3(sv, hv);
                         if (u < 0.0f || u > 1.0f) continue;
@@ -319,7 +321,7 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
                 f3 hv = cross3(d, e2);
                 float a = dot3(e1, hv);
                 if (a > -TRT_EPS && a < TRT_EPS) continue;
-                float f = 1.0f / a;
+                float f = rcp_rn_lane(a);
                 f3 sv = sub(o, v0);
                 float u = f * dot3(sv, hv);
                 if (u < 0.0f || u > 1.0f) continue;
@@ -373,7 +375,7 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
     h.batch = 0;
     if (A.flags & TRT_FLAG_FLOOR) { // shader.comp:302-320
         if (fabsf(d.y) > TRT_EPS) {
-            float t = -(o.y + 4.0f) / d.y;
+            float t = div_rn(-(o.y + 4.0f), d.y);
             if (t > TRT_EPS && t < h.t) {
                 f3 p = add(o, muls(d, t));
                 if (fabsf(p.x) < 10.0f && p.z < -5.0f && p.z > -30.0f) {
@@ -396,7 +398,7 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return;
-    f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:336
+    f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:336
     bool unused = false;
     if (GEOM == 2) trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c);
     else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
@@ -418,7 +420,7 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return false;
-    f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); // shader.comp:377
+    f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:377
     bool occluded = false;
     Hit unused;
     if (GEOM == 2) trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c);
@@ -744,7 +746,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
         acc = (spp == 1u) ? c : add(acc, c);
     }
     cnt.pri += spp;
-    if (spp > 1u) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
+    if (spp > 1u) acc = mk(div_rn(acc.x, (float)spp), div_rn(acc.y, (float)spp), div_rn(acc.z, (float)spp));
     // pow(color, vec3(GAMMA)), shader.comp:598
     const float gx = pow_pos(acc.x, TRT_GAMMA), gy = pow_pos(acc.y, TRT_GAMMA), gz = pow_pos(acc.z, TRT_GAMMA);
     const size_t o = (size_t)k * A.width + x;
@@ -817,7 +819,15 @@ __global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
     // 100 MHz constant clock, written to out32 (tools/waveclock.py)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef TRT_TPW
+    // diagnostic: TRT_TPW tiles per wave, grid-strided (b, b + G, ...; G % 8 == 0 keeps XCDs)
+    for (uint32_t k = 0; k < TRT_TPW; ++k) {
+        const uint32_t b = blockIdx.x + k * gridDim.x;
+        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, b), cnt, lds, slab);
+    }
+#else
     trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
+#endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
     if (threadIdx.x == 0 && A.out32) {
