@@ -38,11 +38,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5", "ref"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight (trt_set_frames_in_flight; the reference's MAX_FRAMES_IN_FLIGHT = 2)")
+    ap.add_argument("--split", type=int, default=0, help="subtree split window (trt_set_subtree_split: 0 auto, 1 off)")
     ap.add_argument("--pmc", default=None, help="PMC summary json (tools/pmc_traffic.py) for roofline.traffic")
     return ap.parse_args()
 
@@ -52,6 +53,8 @@ WORKLOADS = {
     "C3": "1920x1080, spheres + icosphere mesh (5,120 tris / 80 batches), depth 4",
     "C4": "3840x2160, 20 icospheres (102,400 tris / 1,600 batches), depth 4",
     "C5": "3840x2160, C4 scene, 16 jittered spp, depth 4",
+    "ref": "1024x768, the shipped frame: glass + water + ice (37,956 tris / 594 batches), floor, "
+           "7616x3808 seeded envmap, depth 20 (config.hpp:97-101, shader.comp:75-84)",
 }
 
 
@@ -115,7 +118,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
-    scene = S.CONFIGS[args.config]()
+    scene = S.config_reference_default() if args.config == "ref" else S.CONFIGS[args.config]()
     # Weak scaling: rank r renders frame r of a short camera path (camPos drifts along x).
     scene.ubo = S.make_ubo(cam=(0.05 * rank, 0.0, 0.0))
     params = scene.params()
@@ -145,6 +148,7 @@ def main():
     stream = torch.cuda.Stream()
     r.set_stream(stream)
     r.set_frames_in_flight(nfl)
+    r.set_subtree_split(args.split)
     r.render_frames(params, out8, args.warmup)
     torch.cuda.synchronize()
 

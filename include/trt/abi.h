@@ -138,6 +138,22 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
 #define TRT_MAX_FRAMES_IN_FLIGHT 4u
 int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
 
+/* Subtree split (load balance of deep refraction trees).  The reference traces a pixel's whole
+ * Whitted tree depth-first in one invocation (shader.comp:423-583); in mesh scenes at depth 20
+ * a few pixels' trees hold hundreds of segments and one 8x8 tile then runs for milliseconds
+ * while the rest of the GPU idles.  With a window of w depths the frame is traced in depth
+ * windows: a segment at depth k*w is handed to a task queue and traced by any lane of the
+ * next launch.  Rays, hits and counters are unchanged; the colour of a split pixel is the
+ * sum of its subtrees' colours (each summed in the reference's pop order) added in 32.32
+ * fixed point — deterministic, and within a few ulp of the reference's single running sum
+ * (well inside the RGBA8 +-1 bar).  Pixels whose tree stays within the first window are
+ * bit-identical to the unsplit frame.  spp > 1 frames are never split.
+ * window: TRT_SPLIT_AUTO (default: w = 4 for mesh scenes with max_depth >= 8, else off),
+ * TRT_SPLIT_OFF, or 2..5. */
+#define TRT_SPLIT_AUTO 0
+#define TRT_SPLIT_OFF 1
+int trt_set_subtree_split(trt_ctx* ctx, int window);
+
 /* The reference's frame loop (mainLoop -> drawFrame, main.cpp:405-438, 2181-2205) in one
  * call: for each of `nframes` frames, updateUniformBuffer with ubos[i] (or the current UBO
  * when ubos is NULL) and enqueue one trace launch writing out_rgba8 + i * frame_stride

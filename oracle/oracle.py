@@ -24,6 +24,11 @@ MODE_FAST = 0
 MODE_LITERAL = 1
 
 
+def mode_split(window: int) -> int:
+    """Fast mode + the kernel's subtree split (trt_set_subtree_split) with this window."""
+    return 16 + int(window)
+
+
 class OrcScene(ctypes.Structure):
     _fields_ = [
         ("ubo", ctypes.c_void_p),

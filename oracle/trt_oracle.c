@@ -516,12 +516,35 @@ static int seg_alive(float thr, int depth, int max_depth) {
     return depth < max_depth && !(tt < 0.001f);
 }
 
-static v3 cast_ray_fast(const orc_scene* sc, const trt_params* p, v3 orig, v3 dir, counters* cnt) {
+/* Subtree split (the kernel's trt_set_subtree_split, a build extension with no reference
+ * counterpart): with a window W > 0, an alive child at a depth that is a multiple of W is not
+ * pushed; its subtree is folded on its own (recursively, same rule) and its colour added to
+ * the pixel's 32.32 fixed-point sum (integer adds, order-free), exactly as the kernel's task
+ * rounds do.  The fixed-point conversions match the kernel's bit for bit. */
+static int64_t to_fixed(float v) { return (int64_t)((double)v * 4294967296.0); }
+static float from_fixed(int64_t v) { return (float)((double)v * (1.0 / 4294967296.0)); }
+
+static v3 cast_fold(const orc_scene* sc, const trt_params* p, seg_fast root, int W, counters* cnt,
+                    int64_t acc[3], int* spilled);
+
+static void split_child(const orc_scene* sc, const trt_params* p, seg_fast kid, int W, counters* cnt,
+                        int64_t acc[3], int* spilled) {
+    if (!seg_alive(kid.thr, kid.depth, (int)p->max_depth)) return;
+    v3 c = cast_fold(sc, p, kid, W, cnt, acc, spilled);
+    acc[0] += to_fixed(c.x);
+    acc[1] += to_fixed(c.y);
+    acc[2] += to_fixed(c.z);
+    *spilled = 1;
+}
+
+/* The DFS fold of one segment tree in the reference's pop order (unclamped). */
+static v3 cast_fold(const orc_scene* sc, const trt_params* p, seg_fast root, int W, counters* cnt,
+                    int64_t acc[3], int* spilled) {
     const int D = (int)p->max_depth;
     v3 color = mk(0, 0, 0);
     seg_fast deferred[TRT_MAX_DEPTH_LIMIT + 2];
     int nd = 0;
-    seg_fast cur = {orig, dir, 1.0f, 0};
+    seg_fast cur = root;
     for (;;) {
         int have_next = 0;
         seg_fast next;
@@ -566,6 +589,11 @@ static v3 cast_ray_fast(const orc_scene* sc, const trt_params* p, v3 orig, v3 di
                     kid_refl.depth = cur.depth + 1;
                     nkids |= 2;
                 }
+                if (W > 0 && (cur.depth + 1) % W == 0) { /* window edge: split */
+                    if (nkids & 2) split_child(sc, p, kid_refl, W, cnt, acc, spilled);
+                    if (nkids & 1) split_child(sc, p, kid_refr, W, cnt, acc, spilled);
+                    nkids = 0;
+                }
                 /* The reference pushes refraction then reflection and pops the reflection
                  * first; the refraction child waits on the deferred stack. */
                 if (nkids == 3) {
@@ -589,8 +617,28 @@ static v3 cast_ray_fast(const orc_scene* sc, const trt_params* p, v3 orig, v3 di
             break;
         }
     }
-    return mk(fminf(fmaxf(color.x, 0.0f), 1.0f), fminf(fmaxf(color.y, 0.0f), 1.0f),
-              fminf(fmaxf(color.z, 0.0f), 1.0f));
+    return color;
+}
+
+static v3 clamp3(v3 c) {
+    return mk(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f));
+}
+
+/* W = 0: the reference's cast_ray.  W > 0: split pixels' colours are the fixed-point sum of
+ * their subtrees (the kernel's split frame). */
+static v3 cast_ray_fast_w(const orc_scene* sc, const trt_params* p, v3 orig, v3 dir, int W, counters* cnt) {
+    seg_fast root = {orig, dir, 1.0f, 0};
+    int64_t acc[3] = {0, 0, 0};
+    int spilled = 0;
+    v3 c = cast_fold(sc, p, root, W, cnt, acc, &spilled);
+    if (spilled)
+        c = mk(from_fixed(acc[0] + to_fixed(c.x)), from_fixed(acc[1] + to_fixed(c.y)),
+               from_fixed(acc[2] + to_fixed(c.z)));
+    return clamp3(c);
+}
+
+static v3 cast_ray_fast(const orc_scene* sc, const trt_params* p, v3 orig, v3 dir, counters* cnt) {
+    return cast_ray_fast_w(sc, p, orig, dir, 0, cnt);
 }
 
 /* ---- primary rays (main.cpp:1496-1506, shader.comp:592-595) -------------------------- */
@@ -645,6 +693,7 @@ typedef struct {
     const orc_scene* sc;
     const trt_params* p;
     int mode;
+    int split_w; /* ORC_MODE_SPLIT(W): W, else 0 */
     const uint32_t* rows; /* selected image rows, in output order */
     uint32_t nrows;
     float dz;
@@ -670,7 +719,7 @@ static void render_row(job_t* J, uint32_t k, counters* cnt, path_segment* lit_st
         for (uint32_t s = 0; s < spp; ++s) {
             v3 d = primary_dir(p, J->dz, x, y, s);
             v3 c = J->mode == ORC_MODE_LITERAL ? cast_ray_literal(J->sc, p, orig, d, cnt, lit_stack)
-                                               : cast_ray_fast(J->sc, p, orig, d, cnt);
+                                               : cast_ray_fast_w(J->sc, p, orig, d, J->split_w, cnt);
             acc = spp == 1 ? c : add(acc, c);
         }
         if (spp > 1) acc = mk(acc.x / (float)spp, acc.y / (float)spp, acc.z / (float)spp);
@@ -735,7 +784,9 @@ int orc_render(const orc_scene* sc, const trt_params* p, int mode, int nthreads,
     job_t J;
     J.sc = sc;
     J.p = p;
-    J.mode = mode;
+    J.mode = mode >= ORC_MODE_SPLIT(0) ? ORC_MODE_FAST : mode;
+    J.split_w = mode >= ORC_MODE_SPLIT(0) && p->spp <= 1 ? mode - ORC_MODE_SPLIT(0) : 0;
+    if (J.split_w >= (int)p->max_depth) J.split_w = 0; /* the kernel does not split then */
     J.rows = rows;
     J.nrows = nrows;
     J.dz = (float)ray_dz(p);

@@ -16,6 +16,8 @@ extern "C" {
 
 #define ORC_MODE_FAST 0    /* volume stack removed (proven inert) */
 #define ORC_MODE_LITERAL 1 /* shader.comp as written: PathSegment copies + volume stack */
+/* fast mode + the kernel's subtree split with window W (2..5; trt_set_subtree_split) */
+#define ORC_MODE_SPLIT(W) (16 + (W))
 
 typedef struct orc_scene {
     const trt_ubo* ubo;

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--depth", type=int, default=0)
     ap.add_argument("--tag", default="")
     ap.add_argument("--inflight", type=int, default=2, help="frames in flight")
+    ap.add_argument("--split", type=int, default=0, help="subtree split window (0 auto, 1 off, 2..5)")
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=None, help="override trt_params.flags")
     a = ap.parse_args()
     import numpy as np
@@ -51,6 +52,7 @@ def main():
     stream = torch.cuda.Stream()
     r.set_stream(stream)
     r.set_frames_in_flight(a.inflight)
+    r.set_subtree_split(a.split)
     r.render_frames(p, out, 5)
     r.render_frames(p, out, a.frames, timing=True)
     ms = r.frame_times(a.frames)
@@ -68,7 +70,7 @@ def main():
     torch.cuda.synchronize()
     wall_ev = e0.elapsed_time(e1) / a.frames
     rays = st["primary_rays"] + st["secondary_rays"]
-    res = {"tag": a.tag, "inflight": a.inflight, "config": a.config,
+    res = {"tag": a.tag, "inflight": a.inflight, "split": a.split, "config": a.config,
            "size": [p.width, p.height], "depth": p.max_depth, "rays": rays,
            "med_us": round(float(np.median(ms)) * 1e3, 2), "min_us": round(float(ms.min()) * 1e3, 2),
            "Mray_s_kernel": round(rays / (float(np.median(ms)) * 1e-3) / 1e6, 1),

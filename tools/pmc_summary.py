@@ -14,6 +14,7 @@ usage: python tools/pmc_summary.py gpurun_out/pmc profiles/pmc_C2.json
 from __future__ import annotations
 
 import csv
+import re
 import json
 import statistics
 import sys
@@ -28,7 +29,8 @@ def load(pmc_dir: Path) -> dict:
         per_dispatch: dict = defaultdict(dict)
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if "trace_kernel" not in name or ", true>" in name:
+            # the timed frame kernel(s): trace_kernel<CAP, COUNT=false, GEOM, SPLIT>
+            if "trace_kernel" not in name or re.search(r"trace_kernel<\d+, true", name):
                 continue
             d = per_dispatch[r["Dispatch_Id"]]
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])

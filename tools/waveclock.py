@@ -28,7 +28,7 @@ def main():
     import vkcomputeshader_tinyraytracer_amd as trt
     from vkcomputeshader_tinyraytracer_amd import scene as S
 
-    sc = S.CONFIGS[a.config]()
+    sc = S.config_reference_default() if a.config == "ref" else S.CONFIGS[a.config]()
     p = sc.params()
     r = trt.Renderer(0)
     r.upload_scene(sc)

@@ -48,6 +48,7 @@ def lib() -> ctypes.CDLL:
         "trt_update_ubo": (c_int, [vp, vp]),
         "trt_render": (c_int, [vp, ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)]),
         "trt_set_frames_in_flight": (c_int, [vp, c_u32]),
+        "trt_set_subtree_split": (c_int, [vp, c_int]),
         "trt_render_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, vp, ctypes.c_size_t, c_u32]),
         "trt_frame_times": (c_int, [vp, ctypes.POINTER(ctypes.c_float), c_u32]),
         "trt_synchronize": (c_int, [vp]),
@@ -94,6 +95,7 @@ ABI_SYMBOLS = (
     "trt_update_ubo",
     "trt_render",
     "trt_set_frames_in_flight",
+    "trt_set_subtree_split",
     "trt_render_frames",
     "trt_frame_times",
     "trt_synchronize",

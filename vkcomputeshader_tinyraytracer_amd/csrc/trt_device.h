@@ -69,6 +69,26 @@ struct Mat {
 };
 static_assert(sizeof(Mat) == 48, "Mat is 48 B");
 
+// Subtree split (trt_set_subtree_split): a segment at a depth-window edge handed to any lane
+// of a later launch instead of being traced by its pixel's lane.  32 B = 2 x dwordx4.
+struct alignas(16) Task {
+    float o[3];
+    float dx;
+    float dy, dz;
+    float thr;
+    uint32_t px_depth; // output pixel << 5 | depth
+};
+static_assert(sizeof(Task) == 32, "Task is 32 B");
+constexpr uint32_t kTaskDepthBits = 5u;
+constexpr uint32_t kMaxSplitRounds = 16u;
+// Device counters of one frame's split launches (one set per frames-in-flight slot).
+struct SplitCtr {
+    uint32_t spilled;                  // pixels finished by finalize_spilled
+    uint32_t overflow;                 // children traced in place because a queue was full
+    uint32_t produced[kMaxSplitRounds + 1]; // tasks written by launch r (0 = the tile kernel)
+    uint32_t head[kMaxSplitRounds + 1];     // dequeue head of launch r's output (read by r + 1)
+};
+
 struct SphereArg {
     float c[3];
     float r;
@@ -104,6 +124,20 @@ struct KArgs {
     uint32_t top;                     // levels above the batches: 8^top >= nbatch
     uint32_t ntx;                     // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
+    // subtree split: this launch traces depths < split_d1; children at depth split_d1 become
+    // tasks (split_d1 >= max_depth: no split).  split_w: the window (0 = split off).
+    uint32_t split_w, split_d1;
+    uint32_t q_cap;                   // task capacity of each queue
+    uint32_t num_cus;
+    Task* __restrict__ q_out;         // tasks this launch produces
+    const Task* __restrict__ q_in;    // tasks this launch consumes (trace_tasks)
+    Task* __restrict__ q_buf[2];      // the two queues of the slot (ping-pong)
+    uint32_t* __restrict__ q_out_n;   // produced count of q_out
+    const uint32_t* __restrict__ q_in_n;
+    uint32_t* __restrict__ q_in_head;
+    SplitCtr* __restrict__ ctr;
+    unsigned long long* __restrict__ acc; // per output pixel: fixed-point colour (r, g, b, -)
+    uint32_t* __restrict__ spilled;   // output pixels finished by finalize_spilled
 };
 
 } // namespace trt

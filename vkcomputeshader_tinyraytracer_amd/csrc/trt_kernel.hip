@@ -126,6 +126,9 @@ enum : int { HIT_NONE = 0, HIT_FLOOR = 1, HIT_SPHERE = 2, HIT_TRI = 3 };
 // Per-lane work counters (COUNT builds only): the units of trt_stats.
 struct Cnt {
     uint32_t pri = 0, sec = 0, sh = 0, miss = 0, trin = 0, sph = 0, bt = 0, bh = 0, tt = 0, nt = 0;
+#ifdef TRT_DIAG_PIXEL_WORK
+    uint32_t wn = 0, wt = 0, wseg = 0, wmax = 0; // diagnostic: this lane's node visits, tri tests, segments, max nodes/query
+#endif
 };
 
 struct Hit {
@@ -287,15 +290,46 @@ __device__ __forceinline__ bool bvh_box(f3 o, f3 inv, const float* lo, const flo
     return tnear <= tfar && tfar > TRT_EPS && tnear <= best;
 }
 
+// Traversal stack: the first kBvhLdsStack entries in LDS ([entry][lane], conflict-free
+// ds_read/write_b32, ~50-cycle pops), deeper ones in a private (scratch) array.
+#ifndef TRT_BVH_LDS
+#define TRT_BVH_LDS 1
+#endif
+constexpr int kBvhLdsStack = TRT_BVH_LDS ? 24 : 0;
+
+struct BvhStack {
+    uint32_t* lds; // this lane's column
+    uint32_t priv[kBvhStack - kBvhLdsStack];
+    int sp = 0;
+    __device__ __forceinline__ explicit BvhStack(float4* slab)
+        : lds(reinterpret_cast<uint32_t*>(slab) + threadIdx.x) {}
+    __device__ __forceinline__ void push(uint32_t v) {
+        if (sp < kBvhLdsStack) lds[sp * 64] = v;
+        else priv[sp - kBvhLdsStack] = v;
+        ++sp;
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        --sp;
+        return sp < kBvhLdsStack ? lds[sp * 64] : priv[sp - kBvhLdsStack];
+    }
+};
+
 template <bool COUNT, bool SHADOW>
 __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
-                                          float max_dist, Cnt& c) {
-    uint32_t stack[kBvhStack];
-    int sp = 0;
+                                          float max_dist, Cnt& c, float4* slab) {
+    BvhStack stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
+#ifdef TRT_DIAG_PIXEL_WORK
+    uint32_t qn = 0;
+#endif
     for (;;) {
         if (!(node & kBvhLeafBit)) {
+#ifdef TRT_DIAG_PIXEL_WORK
+            ++c.wn;
+            ++qn;
+            c.wmax = max(c.wmax, qn);
+#endif
             const BvhNode nd = A.bvh[node];
             float ta, tb;
             const bool ha = bvh_box(o, inv, nd.lo0, nd.hi0, best, ta);
@@ -303,7 +337,7 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
             if (COUNT) c.nt += 2;
             if (ha && hb) {
                 const bool a_first = ta <= tb;
-                stack[sp++] = a_first ? nd.child[1] : nd.child[0];
+                stack.push(a_first ? nd.child[1] : nd.child[0]);
                 node = a_first ? nd.child[0] : nd.child[1];
                 continue;
             }
@@ -317,6 +351,9 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
             for (uint32_t k = first; k < first + n; ++k) {
                 const TriGeo g = A.bvh_tris[k];
                 if (COUNT) ++c.tt;
+#ifdef TRT_DIAG_PIXEL_WORK
+                ++c.wt;
+#endif
                 const f3 v0 = ld3(g.v0), e1 = ld3(g.e1), e2 = ld3(g.e2);
                 f3 hv = cross3(d, e2);
                 float a = dot3(e1, hv);
@@ -359,9 +396,19 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
                 h.ni = (int)__float_as_uint(g.pad[2]);
             }
         }
-        if (sp == 0) return;
-        node = stack[--sp];
+        if (stack.sp == 0) return;
+        node = stack.pop();
     }
+}
+
+// A ray whose origin or direction is NaN on every axis (e.g. the children and shadow rays of
+// a hit whose smooth normal normalised a zero vector: 0 * inf) makes every slab of
+// ray_aabb_intersect NaN, so the reference's batch test (shader.comp:197-207) fails for every
+// batch and no triangle can be hit.  The conservative hierarchies treat NaN slabs as
+// unconstrained and would visit every node to find that out (a full BVH traversal, ~1 ms):
+// skip the mesh instead — the same (empty) result.
+__device__ __forceinline__ bool ray_misses_all_batches(f3 o, f3 d) {
+    return (o.x != o.x || d.x != d.x) && (o.y != o.y || d.y != d.y) && (o.z != o.z || d.z != d.z);
 }
 
 template <bool COUNT, int GEOM>
@@ -398,9 +445,10 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return;
+    if (GEOM == 2 && ray_misses_all_batches(o, d)) return;
     f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:336
     bool unused = false;
-    if (GEOM == 2) trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c);
+    if (GEOM == 2) trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
     else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
 }
 
@@ -420,10 +468,11 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return false;
+    if (GEOM == 2 && ray_misses_all_batches(o, d)) return false;
     f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:377
     bool occluded = false;
     Hit unused;
-    if (GEOM == 2) trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c);
+    if (GEOM == 2) trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     else walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     return occluded;
 }
@@ -497,6 +546,8 @@ struct Seg {
 // stack lives in LDS laid out [entry][field][lane]: every push/pop is 8 lane-contiguous
 // ds_write_b32/ds_read_b32 (conflict-free), and no VGPRs hold waiting segments.  Deeper
 // trees (max_depth > 5) use a private array (LDS is kept for 16 resident waves per CU).
+// Split launches (trace in depth windows) use a hybrid: the window's entries in LDS and a
+// private tail that only a child traced in place after a full task queue can reach.
 constexpr int LDS_STACK_MAX = 4;
 
 template <int CAP>
@@ -505,27 +556,32 @@ constexpr int lds_stack_floats() { return (CAP >= 1 && CAP <= LDS_STACK_MAX) ? C
 template <int CAP, bool LDS = (CAP <= LDS_STACK_MAX)>
 struct DeferStack;
 
+__device__ __forceinline__ void lds_put(float* p, const Seg& x) {
+    p[0] = x.o.x;
+    p[64] = x.o.y;
+    p[128] = x.o.z;
+    p[192] = x.d.x;
+    p[256] = x.d.y;
+    p[320] = x.d.z;
+    p[384] = x.thr;
+    p[448] = __int_as_float(x.depth);
+}
+__device__ __forceinline__ Seg lds_get(const float* p) {
+    return Seg{mk(p[0], p[64], p[128]), mk(p[192], p[256], p[320]), p[384], __float_as_int(p[448])};
+}
+
 template <int CAP>
 struct DeferStack<CAP, true> {
     float* base; // this lane's column: base[(e * 8 + f) * 64]
     int n = 0;
     __device__ __forceinline__ explicit DeferStack(float* lds) : base(lds + threadIdx.x) {}
     __device__ __forceinline__ void push(const Seg& x) {
-        float* p = base + n * 8 * 64;
-        p[0] = x.o.x;
-        p[64] = x.o.y;
-        p[128] = x.o.z;
-        p[192] = x.d.x;
-        p[256] = x.d.y;
-        p[320] = x.d.z;
-        p[384] = x.thr;
-        p[448] = __int_as_float(x.depth);
+        lds_put(base + n * 8 * 64, x);
         ++n;
     }
     __device__ __forceinline__ Seg pop() {
         --n;
-        const float* p = base + n * 8 * 64;
-        return Seg{mk(p[0], p[64], p[128]), mk(p[192], p[256], p[320]), p[384], __float_as_int(p[448])};
+        return lds_get(base + n * 8 * 64);
     }
 };
 
@@ -538,15 +594,91 @@ struct DeferStack<CAP, false> {
     __device__ __forceinline__ Seg pop() { return s[--n]; }
 };
 
-template <int CAP, bool COUNT, int GEOM>
-__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt, float* lds,
-                                       float4* slab) {
+// CL entries in LDS, then CP private ones.
+template <int CL, int CP>
+struct HybridStack {
+    float* base;
+    Seg s[CP];
+    int n = 0;
+    __device__ __forceinline__ explicit HybridStack(float* lds) : base(lds + threadIdx.x) {}
+    __device__ __forceinline__ void push(const Seg& x) {
+        if (n < CL) lds_put(base + n * 8 * 64, x);
+        else s[n - CL] = x;
+        ++n;
+    }
+    __device__ __forceinline__ Seg pop() {
+        --n;
+        if (n < CL) return lds_get(base + n * 8 * 64);
+        return s[n - CL];
+    }
+};
+
+template <int CAP, bool SPLIT>
+struct StackOf {
+    using type = DeferStack<CAP>;
+};
+template <int CAP>
+struct StackOf<CAP, true> {
+    using type = HybridStack<CAP, (int)TRT_MAX_DEPTH_LIMIT - 1 - CAP>;
+};
+
+// ---- subtree split: task queues ------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Wave-aggregated append of up to two tasks per lane (one atomic per wave).  A task that does
+// not fit the queue is not written and its flag is cleared: the caller traces it in place.
+__device__ __forceinline__ void enqueue2(const KArgs& A, bool& sa, const Seg& a, bool& sb, const Seg& b,
+                                         uint32_t pixel) {
+    const uint64_t ba = __ballot(sa), bb = __ballot(sb);
+    if ((ba | bb) == 0ull) return;
+    const uint32_t na = (uint32_t)__popcll(ba), nb = (uint32_t)__popcll(bb);
+    const uint64_t act = __ballot(true);
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    uint32_t base = 0;
+    if ((int)threadIdx.x == leader) base = atomicAdd(A.q_out_n, na + nb);
+    base = __shfl(base, leader, 64);
+    const uint32_t ia = base + lane_rank(ba), ib = base + na + lane_rank(bb);
+    auto put = [&](bool& f, uint32_t i, const Seg& x) {
+        if (!f) return;
+        if (i >= A.q_cap) {
+            f = false;
+            atomicAdd(&A.ctr->overflow, 1u);
+            return;
+        }
+        float4* q = reinterpret_cast<float4*>(A.q_out + i);
+        q[0] = make_float4(x.o.x, x.o.y, x.o.z, x.d.x);
+        q[1] = make_float4(x.d.y, x.d.z, x.thr, __uint_as_float((pixel << kTaskDepthBits) | (uint32_t)x.depth));
+    };
+    put(sa, ia, a);
+    put(sb, ib, b);
+}
+
+// Colours of split pixels are summed in 32.32 fixed point (integer adds: the same result in
+// any order); finalize_spilled converts back.
+__device__ __forceinline__ unsigned long long to_fixed(float v) {
+    return (unsigned long long)(long long)((double)v * 4294967296.0);
+}
+__device__ __forceinline__ float from_fixed(unsigned long long v) {
+    return (float)((double)(long long)v * (1.0 / 4294967296.0));
+}
+
+// The DFS of one segment tree (root = a primary ray, or a task of a split launch).  Returns
+// the unclamped colour sum in the reference's pop order.  SPLIT: children at depth
+// >= A.split_d1 are handed to the task queue (`spilled` is set) instead of being traced.
+template <int CAP, bool COUNT, int GEOM, bool SPLIT>
+__device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float* lds, float4* slab,
+                                       uint32_t pixel, bool& spilled) {
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    DeferStack<CAP> stk(lds);
-    Seg cur{orig, dir, 1.0f, 0};
+    typename StackOf<CAP, SPLIT>::type stk(lds);
     for (;;) {
         if (COUNT && cur.depth > 0) ++cnt.sec;
+#ifdef TRT_DIAG_PIXEL_WORK
+        ++cnt.wseg;
+#endif
 #ifdef TRT_PRIO
         if (cur.depth > 0) __builtin_amdgcn_s_setprio(TRT_PRIO);
 #endif
@@ -653,6 +785,13 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
                 float tt = (refl.thr * refl.thr + refl.thr * refl.thr) + refl.thr * refl.thr;
                 mk_refl = cd < D && !(tt < 0.001f);
             }
+            if (SPLIT && cd >= (int)A.split_d1) { // window edge: both children become tasks
+                bool sa = mk_refl, sb = mk_refr;
+                enqueue2(A, sa, refl, sb, refr, pixel);
+                if (sa) mk_refl = false;
+                if (sb) mk_refr = false;
+                spilled = spilled || sa || sb;
+            }
             // Reference pushes refraction then reflection and pops reflection first.
             if (mk_refl) {
                 if (mk_refr) stk.push(refr);
@@ -671,7 +810,15 @@ __device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt
             break;
         }
     }
-    return mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)); // shader.comp:582
+    return color;
+}
+
+template <int CAP, bool COUNT, int GEOM>
+__device__ __forceinline__ f3 cast_ray(const KArgs& A, f3 orig, f3 dir, Cnt& cnt, float* lds,
+                                       float4* slab) {
+    bool unused = false;
+    const f3 c = cast_seg<CAP, COUNT, GEOM, false>(A, Seg{orig, dir, 1.0f, 0}, cnt, lds, slab, 0u, unused);
+    return mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)); // shader.comp:582
 }
 
 // ---- primary rays (main.cpp:1496-1506 on the host; shader.comp:592-595) -----------------
@@ -724,32 +871,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
     return x;
 }
 
-// One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.
-template <int CAP, bool COUNT, int GEOM>
-__device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
-    const uint32_t lane = threadIdx.x;
-    if (tile >= A.ntiles) return;
-    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
-    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
-    if (x >= A.width || k >= A.rows) return;
-#ifdef TRT_DIAG_TRIVIAL
-    if (A.out8) A.out8[(size_t)k * A.width + x] = 0xff000000u | x; // diagnostic: launch + store only
-    return;
-#endif
-    const uint32_t y = band_row(A, k);
-    const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
-    const uint32_t spp = A.spp ? A.spp : 1u;
-    f3 acc = mk(0.0f, 0.0f, 0.0f);
-    for (uint32_t s = 0; s < spp; ++s) {
-        f3 d = primary_dir(A, x, y, s);
-        f3 c = cast_ray<CAP, COUNT, GEOM>(A, orig, d, cnt, lds, slab);
-        acc = (spp == 1u) ? c : add(acc, c);
-    }
-    cnt.pri += spp;
-    if (spp > 1u) acc = mk(div_rn(acc.x, (float)spp), div_rn(acc.y, (float)spp), div_rn(acc.z, (float)spp));
-    // pow(color, vec3(GAMMA)), shader.comp:598
-    const float gx = pow_pos(acc.x, TRT_GAMMA), gy = pow_pos(acc.y, TRT_GAMMA), gz = pow_pos(acc.z, TRT_GAMMA);
-    const size_t o = (size_t)k * A.width + x;
+// Gamma (shader.comp:598) and the dual store (rayOut binding 2, storage image binding 3) of
+// output pixel o; `c` is the clamped colour.
+__device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
+    const float gx = pow_pos(c.x, TRT_GAMMA), gy = pow_pos(c.y, TRT_GAMMA), gz = pow_pos(c.z, TRT_GAMMA);
 #ifdef TRT_DIAG_WAVE_CLOCK
     if (false) // out32 carries the workgroup clock records
 #else
@@ -770,6 +895,62 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
         uint32_t b = (uint32_t)floorf(ez * 255.0f + 0.5f);
         A.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
     }
+}
+
+// One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.  SPLIT
+// (spp == 1 only): a pixel whose tree handed subtrees to the task queue parks its partial
+// colour in A.acc and is finished by finalize_spilled.
+template <int CAP, bool COUNT, int GEOM, bool SPLIT>
+__device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
+    const uint32_t lane = threadIdx.x;
+    if (tile >= A.ntiles) return;
+    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
+    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    if (x >= A.width || k >= A.rows) return;
+#ifdef TRT_DIAG_TRIVIAL
+    if (A.out8) A.out8[(size_t)k * A.width + x] = 0xff000000u | x; // diagnostic: launch + store only
+    return;
+#endif
+    const uint32_t y = band_row(A, k);
+    const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
+    const size_t o = (size_t)k * A.width + x;
+    if (SPLIT) {
+        bool spilled = false;
+        const f3 c = cast_seg<CAP, COUNT, GEOM, true>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds,
+                                                      slab, (uint32_t)o, spilled);
+        cnt.pri += 1;
+        const uint64_t sp = __ballot(spilled);
+        if (spilled) {
+            unsigned long long* a = A.acc + 4 * o;
+            a[0] = to_fixed(c.x);
+            a[1] = to_fixed(c.y);
+            a[2] = to_fixed(c.z);
+        }
+        if (sp) {
+            const int leader = __ffsll((unsigned long long)sp) - 1;
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(&A.ctr->spilled, (uint32_t)__popcll(sp));
+            base = __shfl(base, leader, 64);
+            if (spilled) A.spilled[base + lane_rank(sp)] = (uint32_t)o;
+        }
+        if (!spilled) store_pixel(A, o, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)));
+        return;
+    }
+    const uint32_t spp = A.spp ? A.spp : 1u;
+    f3 acc = mk(0.0f, 0.0f, 0.0f);
+    for (uint32_t s = 0; s < spp; ++s) {
+        f3 d = primary_dir(A, x, y, s);
+        f3 c = cast_ray<CAP, COUNT, GEOM>(A, orig, d, cnt, lds, slab);
+        acc = (spp == 1u) ? c : add(acc, c);
+    }
+    cnt.pri += spp;
+    if (spp > 1u) acc = mk(div_rn(acc.x, (float)spp), div_rn(acc.y, (float)spp), div_rn(acc.z, (float)spp));
+#ifdef TRT_DIAG_PIXEL_WORK
+    // diagnostic: out32 = (node visits, triangle tests, segments, max node visits of one query)
+    if (A.out32) reinterpret_cast<float4*>(A.out32)[o] = make_float4((float)cnt.wn, (float)cnt.wt, (float)cnt.wseg, (float)cnt.wmax);
+    return;
+#endif
+    store_pixel(A, o, acc);
 }
 
 // Blocks b and b+8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md): give each XCD
@@ -809,10 +990,21 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
 #ifndef TRT_WAVES
 #define TRT_WAVES 1
 #endif
-template <int CAP, bool COUNT, int GEOM>
+
+__device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
+    const uint32_t v[10] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt};
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        unsigned long long w = wave_sum((unsigned long long)v[i]);
+        if (threadIdx.x == 0) atomicAdd(&A.counters[i], w);
+    }
+}
+
+template <int CAP, bool COUNT, int GEOM, bool SPLIT>
 __global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
-    __shared__ float4 slab[GEOM == 1 ? 64 * 3 : 1]; // one batch slab: 64 x (v0, e1, e2)
+    // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
+    __shared__ float4 slab[GEOM == 1 ? 64 * 3 : GEOM == 2 ? (kBvhLdsStack > 0 ? kBvhLdsStack * 16 : 1) : 1];
     Cnt cnt;
 #ifdef TRT_DIAG_WAVE_CLOCK
     // diagnostic: per-workgroup (tile | xcc << 28, start lo, duration, start hi) of the
@@ -823,10 +1015,10 @@ __global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
     // diagnostic: TRT_TPW tiles per wave, grid-strided (b, b + G, ...; G % 8 == 0 keeps XCDs)
     for (uint32_t k = 0; k < TRT_TPW; ++k) {
         const uint32_t b = blockIdx.x + k * gridDim.x;
-        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, b), cnt, lds, slab);
+        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, b), cnt, lds, slab);
     }
 #else
-    trace_tile<CAP, COUNT, GEOM>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
+    trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
 #endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
@@ -841,18 +1033,80 @@ __global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
         rec[3] = (uint32_t)(t_start >> 32);
     }
 #endif
-    if (COUNT) {
-        const uint32_t v[10] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt};
-#pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            unsigned long long w = wave_sum((unsigned long long)v[i]);
-            if (threadIdx.x == 0) atomicAdd(&A.counters[i], w);
+    if (COUNT) flush_counts(A, cnt);
+}
+
+// One round of a split frame: persistent waves pull 64 tasks at a time (one atomic per wave)
+// from the previous launch's queue, trace each task's subtree within the depth window (its
+// window-edge children go to the next queue) and add the subtree's colour to its pixel's
+// fixed-point sum.  Every wave leaves once the queue is drained.
+template <int CAP, bool COUNT, int GEOM>
+__global__ __launch_bounds__(64, TRT_WAVES) void trace_tasks(KArgs A) {
+    __shared__ float lds[lds_stack_floats<CAP>()];
+    __shared__ float4 slab[GEOM == 1 ? 64 * 3 : GEOM == 2 ? (kBvhLdsStack > 0 ? kBvhLdsStack * 16 : 1) : 1];
+    Cnt cnt;
+    const uint32_t n = min(*A.q_in_n, A.q_cap);
+    for (;;) {
+        uint32_t base = 0;
+        if (threadIdx.x == 0) base = atomicAdd(A.q_in_head, 64u);
+        base = __shfl(base, 0, 64);
+        if (base >= n) break;
+        const uint32_t t = base + threadIdx.x;
+        if (t < n) {
+            const float4* q = reinterpret_cast<const float4*>(A.q_in + t);
+            const float4 a = q[0], b = q[1];
+            const uint32_t pd = __float_as_uint(b.w);
+            const uint32_t pixel = pd >> kTaskDepthBits;
+            const Seg root{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z, (int)(pd & ((1u << kTaskDepthBits) - 1u))};
+            bool spilled = false;
+            const f3 c = cast_seg<CAP, COUNT, GEOM, true>(A, root, cnt, lds, slab, pixel, spilled);
+            unsigned long long* acc = A.acc + 4 * (size_t)pixel;
+            atomicAdd(acc + 0, to_fixed(c.x));
+            atomicAdd(acc + 1, to_fixed(c.y));
+            atomicAdd(acc + 2, to_fixed(c.z));
         }
+    }
+    if (COUNT) flush_counts(A, cnt);
+}
+
+// Finishes the pixels whose trees were split: fixed-point sum -> clamp -> gamma -> store.
+__global__ __launch_bounds__(256) void finalize_spilled(KArgs A) {
+    const uint32_t n = A.ctr->spilled;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t o = A.spilled[i];
+        const unsigned long long* acc = A.acc + 4 * (size_t)o;
+        const f3 c = mk(from_fixed(acc[0]), from_fixed(acc[1]), from_fixed(acc[2]));
+        store_pixel(A, o, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)));
     }
 }
 
+template <int CAP, bool COUNT, int GEOM>
+static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid) {
+    KArgs A = A0;
+    const uint32_t D = A.max_depth, W = A.split_w;
+    A.split_d1 = W;
+    A.q_out = A.q_buf[0];
+    A.q_out_n = &A.ctr->produced[0];
+    hipLaunchKernelGGL((trace_kernel<CAP, COUNT, GEOM, true>), grid, dim3(64), 0, stream, A);
+    uint32_t r = 1;
+    for (uint32_t d0 = W; d0 < D && r <= kMaxSplitRounds; d0 += W, ++r) {
+        A.split_d1 = d0 + W;
+        A.q_in = A.q_buf[(r - 1) & 1];
+        A.q_in_n = &A.ctr->produced[r - 1];
+        A.q_in_head = &A.ctr->head[r - 1];
+        A.q_out = A.q_buf[r & 1];
+        A.q_out_n = &A.ctr->produced[r];
+        // persistent: 3 one-wave workgroups per SIMD (the mesh kernels' occupancy)
+        hipLaunchKernelGGL((trace_tasks<CAP, COUNT, GEOM>), dim3(A.num_cus * 12), dim3(64), 0, stream, A);
+    }
+    hipLaunchKernelGGL(finalize_spilled, dim3(A.num_cus), dim3(256), 0, stream, A);
+}
+
 // Launch helper: picks the deferred-stack capacity from max_depth (children are made only
-// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once).
+// for depth+1 < max_depth, so at most max_depth-1 refraction children wait at once; inside a
+// split window of w depths at most w - 1 do, so split launches keep w - 1 in LDS).  With a
+// split window (A.split_w in [2, 5], spp == 1, max_depth > window) the frame is traced in
+// depth windows: the tile kernel, one trace_tasks round per further window, finalize_spilled.
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const uint32_t D = A.max_depth;
 #ifdef TRT_TPW
@@ -861,10 +1115,34 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const dim3 grid(A.ntiles), block(64);
 #endif
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? 2 : 1;
-#define TRT_LAUNCH_G(CAP, G)                                                                      \
-    do {                                                                                          \
-        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G>), grid, block, 0, stream, A);   \
-        else hipLaunchKernelGGL((trace_kernel<CAP, false, G>), grid, block, 0, stream, A);        \
+    if (A.split_w >= 2 && A.split_w <= 5 && A.split_w < D && A.spp <= 1 && A.acc && A.ctr) {
+        hipError_t e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
+        if (e != hipSuccess) return e;
+#define TRT_SPLIT_G(CAP, G)                                                 \
+    do {                                                                    \
+        if (count) launch_split<CAP, true, G>(A, stream, grid);            \
+        else launch_split<CAP, false, G>(A, stream, grid);                 \
+    } while (0)
+#define TRT_SPLIT(CAP)                            \
+    do {                                          \
+        if (geom == 0) TRT_SPLIT_G(CAP, 0);       \
+        else if (geom == 1) TRT_SPLIT_G(CAP, 1);  \
+        else TRT_SPLIT_G(CAP, 2);                 \
+    } while (0)
+        switch (A.split_w) {
+        case 2: TRT_SPLIT(1); break;
+        case 3: TRT_SPLIT(2); break;
+        case 4: TRT_SPLIT(3); break;
+        default: TRT_SPLIT(4); break;
+        }
+#undef TRT_SPLIT
+#undef TRT_SPLIT_G
+        return hipGetLastError();
+    }
+#define TRT_LAUNCH_G(CAP, G)                                                                             \
+    do {                                                                                                 \
+        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G, false>), grid, block, 0, stream, A);   \
+        else hipLaunchKernelGGL((trace_kernel<CAP, false, G, false>), grid, block, 0, stream, A);        \
     } while (0)
 #define TRT_LAUNCH(CAP)                          \
     do {                                         \

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <cstring>
 #include <map>
@@ -65,6 +66,19 @@ struct trt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
     uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
+    int subtree_split = TRT_SPLIT_AUTO;
+    // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
+    // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
+    // the counters.
+    struct SplitBufs {
+        trt::Task* q[2] = {nullptr, nullptr};
+        unsigned long long* acc = nullptr;
+        uint32_t* spilled = nullptr;
+        trt::SplitCtr* ctr = nullptr;
+        size_t npx = 0;  // pixels the buffers hold
+        uint32_t cap = 0; // tasks per queue
+    };
+    SplitBufs split[TRT_MAX_FRAMES_IN_FLIGHT];
     std::vector<hipStream_t> aux; // frames-in-flight streams (frame i -> stream i % n)
     std::vector<hipEvent_t> aux_ev;
     hipEvent_t fork_ev = nullptr;
@@ -224,6 +238,13 @@ int trt_destroy(trt_ctx* c) {
     (void)hipFree(c->d_rays);
     (void)hipFree(c->d_counters);
     for (hipEvent_t e : c->fev) (void)hipEventDestroy(e);
+    for (auto& b : c->split) {
+        (void)hipFree(b.q[0]);
+        (void)hipFree(b.q[1]);
+        (void)hipFree(b.acc);
+        (void)hipFree(b.spilled);
+        (void)hipFree(b.ctr);
+    }
     for (hipStream_t s : c->aux) {
         (void)hipStreamSynchronize(s);
         (void)hipStreamDestroy(s);
@@ -250,6 +271,14 @@ int trt_set_frames_in_flight(trt_ctx* c, uint32_t n) {
     if (n < 1 || n > TRT_MAX_FRAMES_IN_FLIGHT)
         return fail(c, TRT_ERR_INVALID, "trt_set_frames_in_flight: n must be in [1, TRT_MAX_FRAMES_IN_FLIGHT]");
     c->frames_in_flight = n;
+    return TRT_OK;
+}
+
+int trt_set_subtree_split(trt_ctx* c, int window) {
+    if (!c) return TRT_ERR_INVALID;
+    if (window != TRT_SPLIT_AUTO && window != TRT_SPLIT_OFF && (window < 2 || window > 5))
+        return fail(c, TRT_ERR_INVALID, "trt_set_subtree_split: window must be 0 (auto), 1 (off) or 2..5");
+    c->subtree_split = window;
     return TRT_OK;
 }
 
@@ -486,6 +515,67 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.ntiles = A.ntx * ((A.rows + 7u) / 8u);
 }
 
+// The subtree-split window of a frame: 0 = off.  Auto: scenes with meshes (whose deep
+// refraction trees make a few tiles run for milliseconds) with max_depth above the window.
+uint32_t split_window(const trt_ctx* c, const trt_params* p) {
+    const uint32_t D = p->max_depth;
+    if ((p->spp > 1) || c->subtree_split == TRT_SPLIT_OFF) return 0;
+    if ((size_t)trt_output_rows(p) * p->width >= (1u << (32 - trt::kTaskDepthBits))) return 0;
+    uint32_t w;
+    if (c->subtree_split == TRT_SPLIT_AUTO) {
+        // measured (profiles/r01_split_sweep.log): -10..-16 % on the shipped depth-20 frame with
+        // w = 4; +0..+25 % on depth-4 mesh frames (C3/C4) for any window, so only deep trees
+        if (c->nbatch == 0 || D < 8) return 0;
+        w = 4u;
+    } else {
+        w = (uint32_t)c->subtree_split;
+    }
+    return w < D ? w : 0u;
+}
+
+// Allocates slot `slot`'s split scratch for this frame size and fills A's split fields.
+int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
+    A.split_w = split_window(c, p);
+    A.split_d1 = A.max_depth;
+    A.num_cus = c->num_cus;
+    if (!A.split_w) return TRT_OK;
+    auto& b = c->split[slot];
+    const size_t npx = (size_t)trt_output_rows(p) * p->width;
+    if (npx > b.npx) {
+        // queue capacity: 4 tasks per pixel per window edge (a full queue is not an error: the
+        // child is traced in place, SplitCtr::overflow counts it)
+        const size_t cap = std::min<size_t>(std::max<size_t>(4 * npx, 1u << 16), 1u << 28);
+        for (auto* q : b.q) (void)hipFree(q);
+        (void)hipFree(b.acc);
+        (void)hipFree(b.spilled);
+        b = {};
+        hipError_t e = hipMalloc((void**)&b.q[0], cap * sizeof(trt::Task));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.q[1], cap * sizeof(trt::Task));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.acc, npx * 4 * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.spilled, npx * sizeof(uint32_t));
+        if (e == hipSuccess && !b.ctr) e = hipMalloc((void**)&b.ctr, sizeof(trt::SplitCtr));
+        if (e != hipSuccess) {
+            for (auto* q : b.q) (void)hipFree(q);
+            (void)hipFree(b.acc);
+            (void)hipFree(b.spilled);
+            (void)hipFree(b.ctr);
+            b = {};
+            return hip_fail(c, e, "alloc subtree-split buffers");
+        }
+        b.npx = npx;
+        b.cap = (uint32_t)cap;
+    }
+    A.q_buf[0] = b.q[0];
+    A.q_buf[1] = b.q[1];
+    A.q_cap = b.cap;
+    // test hook: a tiny queue exercises the in-place fallback (tests/test_gpu_split.py)
+    if (const char* e = std::getenv("TRT_SPLIT_QCAP")) A.q_cap = std::min<uint32_t>(A.q_cap, (uint32_t)std::strtoul(e, nullptr, 10));
+    A.acc = b.acc;
+    A.spilled = b.spilled;
+    A.ctr = b.ctr;
+    return TRT_OK;
+}
+
 } // namespace
 
 extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
@@ -540,6 +630,7 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
             fill_ubo_args(A, c->ubo);
         }
         hipStream_t st = sv[i % nfl];
+        if ((rc = prepare_split(c, p, A, i % nfl)) != TRT_OK) return rc;
         A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
         const bool timed = timing && i % every == 0;
         const size_t k = 2 * (size_t)(i / every);
@@ -611,6 +702,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
             A.out32 = reinterpret_cast<float*>(c->d_out32);
         }
     }
+    if ((rc = prepare_split(c, p, A, 0)) != TRT_OK) return rc;
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));

@@ -61,6 +61,10 @@ class Renderer:
         reference's MAX_FRAMES_IN_FLIGHT = 2, main.cpp:45)."""
         self._check(self._L.trt_set_frames_in_flight(self._h, int(n)))
 
+    def set_subtree_split(self, window: int) -> None:
+        """trt_set_subtree_split: 0 = auto (default), 1 = off, 2..5 = depth window."""
+        self._check(self._L.trt_set_subtree_split(self._h, int(window)))
+
     def set_stream(self, stream) -> None:
         """`stream`: a torch.cuda.Stream (not the legacy default stream), a raw hipStream_t
         int, or None (the context's own stream)."""
