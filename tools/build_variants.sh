@@ -39,6 +39,7 @@ for v in "$@"; do
         tpw2) variant tpw2 -DTRT_TPW=2 ;;
         fmexec) variant fmexec -DTRT_FM_EXEC_BRANCH ;;
         nolds) variant nolds -DTRT_BVH_LDS=0 ;;
+        bvh2) variant bvh2 -DTRT_BVH_WIDTH=2 ;;
         work) variant work -DTRT_DIAG_PIXEL_WORK ;;
         prev) # the kernel of git revision $PREV (default HEAD), for A/B against the work tree
             git -C "$ROOT" show "${PREV:-HEAD}:vkcomputeshader_tinyraytracer_amd/csrc/trt_kernel.hip" > "$SRC/.prev_kernel.hip"

@@ -241,4 +241,97 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
     return true;
 }
 
+// Collapses the BVH2 into 4-wide nodes: a BVH4 node's children are the BVH2 subtrees reached
+// by repeatedly opening the inner child of largest surface area (up to 4).  Leaves keep their
+// encoding (same leaf triangle array).  Node 0 is the root.  Returns the traversal stack the
+// 4-wide walk can need: the largest sum over a root-to-leaf path of (children - 1), since a
+// visit pushes at most all but one of its children.
+uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4) {
+    b4.clear();
+    if (b2.empty()) return 0;
+    struct Ref {
+        uint32_t ref;
+        Box box;
+    };
+    auto area = [](const Box& b) { return b.area(); };
+    // children of BVH2 node n as refs with boxes
+    auto kids = [&](uint32_t n, Ref out[2]) {
+        const BvhNode& nd = b2[n];
+        for (int k = 0; k < 3; ++k) {
+            out[0].box.lo[k] = nd.lo0[k];
+            out[0].box.hi[k] = nd.hi0[k];
+            out[1].box.lo[k] = nd.lo1[k];
+            out[1].box.hi[k] = nd.hi1[k];
+        }
+        out[0].ref = nd.child[0];
+        out[1].ref = nd.child[1];
+    };
+    // BFS over BVH2 inner nodes that become BVH4 nodes
+    std::vector<uint32_t> todo{0u};
+    b4.reserve(b2.size() / 2 + 1);
+    std::vector<uint32_t> index_of(b2.size(), kBvh4None);
+    index_of[0] = 0;
+    b4.emplace_back();
+    for (size_t qi = 0; qi < todo.size(); ++qi) {
+        const uint32_t n2 = todo[qi];
+        Ref set[4];
+        int cnt = 2;
+        kids(n2, set);
+        for (;;) { // open the largest inner child while there is room
+            int best = -1;
+            float ba = -1.0f;
+            for (int i = 0; i < cnt; ++i)
+                if (!(set[i].ref & kBvhLeafBit) && area(set[i].box) > ba) {
+                    ba = area(set[i].box);
+                    best = i;
+                }
+            if (best < 0 || cnt == 4) break;
+            Ref two[2];
+            kids(set[best].ref, two);
+            set[best] = two[0];
+            set[cnt++] = two[1];
+        }
+        Bvh4Node nd;
+        for (int i = 0; i < 4; ++i) {
+            if (i < cnt) {
+                nd.lox[i] = set[i].box.lo[0];
+                nd.loy[i] = set[i].box.lo[1];
+                nd.loz[i] = set[i].box.lo[2];
+                nd.hix[i] = set[i].box.hi[0];
+                nd.hiy[i] = set[i].box.hi[1];
+                nd.hiz[i] = set[i].box.hi[2];
+                uint32_t r = set[i].ref;
+                if (!(r & kBvhLeafBit)) {
+                    if (index_of[r] == kBvh4None) {
+                        index_of[r] = (uint32_t)b4.size();
+                        b4.emplace_back();
+                        todo.push_back(r);
+                    }
+                    r = index_of[r];
+                }
+                nd.child[i] = r;
+            } else {
+                nd.lox[i] = nd.loy[i] = nd.loz[i] = 0.0f;
+                nd.hix[i] = nd.hiy[i] = nd.hiz[i] = 0.0f;
+                nd.child[i] = kBvh4None;
+            }
+            nd.pad[i] = 0;
+        }
+        b4[index_of[n2]] = nd;
+    }
+    // stack bound, children before parents reversed: nodes were appended in BFS order
+    std::vector<uint32_t> need(b4.size(), 0);
+    for (size_t i = b4.size(); i-- > 0;) {
+        const Bvh4Node& nd = b4[i];
+        uint32_t cnt = 0, deepest = 0;
+        for (int k = 0; k < 4; ++k) {
+            if (nd.child[k] == kBvh4None) continue;
+            ++cnt;
+            if (!(nd.child[k] & kBvhLeafBit)) deepest = std::max(deepest, need[nd.child[k]]);
+        }
+        need[i] = (cnt ? cnt - 1 : 0) + deepest;
+    }
+    return need.empty() ? 0 : need[0];
+}
+
 } // namespace trt

@@ -60,6 +60,18 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
 
+// 4-wide node collapsed from the BVH2 (bvh_build.cpp): one visit resolves two BVH2 levels,
+// halving the dependent node fetches per query.  Child boxes SoA (lo_x[4] ...), 128 B = 8 x
+// dwordx4; an unused slot has child == kBvh4None.
+constexpr uint32_t kBvh4None = 0xFFFFFFFFu;
+struct alignas(16) Bvh4Node {
+    float lox[4], loy[4], loz[4];
+    float hix[4], hiy[4], hiz[4];
+    uint32_t child[4];
+    uint32_t pad[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node is 128 B");
+
 struct Mat {
     float albedo[4];
     float kd[3];
@@ -118,6 +130,7 @@ struct KArgs {
     float* __restrict__ out32;         // float4 per pixel, or null
     unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
     const BvhNode* __restrict__ bvh;  // per-lane BVH over triangles, or null (batch walk)
+    const Bvh4Node* __restrict__ bvh4; // the same BVH collapsed to 4-wide nodes
     const TriGeo* __restrict__ bvh_tris; // BVH-ordered geometry; pad = (triangle, batch, ni)
     const float4* __restrict__ nodes; // batch hierarchy: per node (lo.xyz, -), (hi.xyz, -)
     uint32_t node_off[11];            // first node of level L (L = 1..top) in `nodes`

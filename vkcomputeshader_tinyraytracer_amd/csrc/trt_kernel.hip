@@ -401,6 +401,129 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
     }
 }
 
+// Tests the leaf `node` (1-8 triangles of the BVH-ordered array).  SHADOW: returns true when
+// an accepted candidate occludes.  The next triangle's record is loaded before the current
+// one is tested (one exposed load latency per leaf instead of one per triangle).
+template <bool COUNT, bool SHADOW>
+__device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3 d, f3 inv, Hit& h,
+                                         float max_dist, float& best, Cnt& c) {
+    const uint32_t first = node & kBvhFirstMask;
+    const uint32_t n = ((node >> kBvhCountShift) & 15u) + 1u;
+    TriGeo g = A.bvh_tris[first];
+    for (uint32_t k = first; k < first + n; ++k) {
+        const TriGeo cur = g;
+        if (k + 1 < first + n) g = A.bvh_tris[k + 1];
+        if (COUNT) ++c.tt;
+#ifdef TRT_DIAG_PIXEL_WORK
+        ++c.wt;
+#endif
+        const f3 v0 = ld3(cur.v0), e1 = ld3(cur.e1), e2 = ld3(cur.e2);
+        f3 hv = cross3(d, e2);
+        float a = dot3(e1, hv);
+        if (a > -TRT_EPS && a < TRT_EPS) continue;
+        float f = rcp_rn_lane(a);
+        f3 sv = sub(o, v0);
+        float u = f * dot3(sv, hv);
+        if (u < 0.0f || u > 1.0f) continue;
+        f3 q = cross3(sv, e1);
+        float v = f * dot3(d, q);
+        if (v < 0.0f || u + v > 1.0f) continue;
+        float t = f * dot3(e2, q);
+        if (t <= TRT_EPS) continue;
+        const uint32_t tri = __float_as_uint(cur.pad[0]), batch = __float_as_uint(cur.pad[1]);
+        if (SHADOW) {
+            if (!(t < max_dist)) continue;
+        } else {
+            const bool better = t < best || (t == best && h.kind == HIT_TRI &&
+                                             (batch < h.batch || (batch == h.batch && (int)tri < h.idx)));
+            if (!better) continue;
+        }
+        const BatchRec rec = A.batches[batch]; // the reference's gate for this triangle
+        const bool pass = aabb_hit(o, inv, rec.bmin, rec.bmax);
+        if (COUNT) {
+            ++c.bt;
+            c.bh += pass ? 1u : 0u;
+        }
+        if (!pass) continue;
+        if (SHADOW) return true;
+        best = t;
+        h.t = t;
+        h.kind = HIT_TRI;
+        h.idx = (int)tri;
+        h.batch = batch;
+        h.u = u;
+        h.v = v;
+        h.ni = (int)__float_as_uint(cur.pad[2]);
+    }
+    return false;
+}
+
+#ifndef TRT_BVH_WIDTH
+#define TRT_BVH_WIDTH 4
+#endif
+
+// 4-wide traversal: the four child boxes of a node in one 128-B fetch, entered nearest first
+// (the others pushed farthest first, so the next pop is the next nearest).
+template <bool COUNT, bool SHADOW>
+__device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
+                                           float max_dist, Cnt& c, float4* slab) {
+    BvhStack stack(slab);
+    uint32_t node = 0;
+    float best = SHADOW ? max_dist : h.t;
+    for (;;) {
+        if (!(node & kBvhLeafBit)) {
+            const float4* p = reinterpret_cast<const float4*>(A.bvh4 + node);
+            const float4 lx = p[0], ly = p[1], lz = p[2], hx = p[3], hy = p[4], hz = p[5];
+            const uint4 ch = reinterpret_cast<const uint4*>(p)[6];
+#ifdef TRT_DIAG_PIXEL_WORK
+            ++c.wn;
+#endif
+            float t[4];
+            uint32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
+            const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
+            const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
+            int nh = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float tn;
+                const bool ok = r[i] != kBvh4None && bvh_box(o, inv, lo[i], hi[i], best, tn);
+                t[i] = ok ? tn : __builtin_huge_valf();
+                nh += ok ? 1 : 0;
+            }
+            if (COUNT) c.nt += (ch.x != kBvh4None) + (ch.y != kBvh4None) + (ch.z != kBvh4None) + (ch.w != kBvh4None);
+            if (nh > 0) {
+                // sorting network on (t, ref): ascending t, misses (t = inf) last
+#define TRT_CSWAP(a, b)                                   \
+    do {                                                  \
+        const bool sw = t[b] < t[a];                      \
+        const float ta = t[a], tb = t[b];                 \
+        const uint32_t ra = r[a], rb = r[b];              \
+        t[a] = sw ? tb : ta;                              \
+        t[b] = sw ? ta : tb;                              \
+        r[a] = sw ? rb : ra;                              \
+        r[b] = sw ? ra : rb;                              \
+    } while (0)
+                TRT_CSWAP(0, 1);
+                TRT_CSWAP(2, 3);
+                TRT_CSWAP(0, 2);
+                TRT_CSWAP(1, 3);
+                TRT_CSWAP(1, 2);
+#undef TRT_CSWAP
+                if (nh > 3) stack.push(r[3]);
+                if (nh > 2) stack.push(r[2]);
+                if (nh > 1) stack.push(r[1]);
+                node = r[0];
+                continue;
+            }
+        } else if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
+            occluded = true;
+            return;
+        }
+        if (stack.sp == 0) return;
+        node = stack.pop();
+    }
+}
+
 // A ray whose origin or direction is NaN on every axis (e.g. the children and shadow rays of
 // a hit whose smooth normal normalised a zero vector: 0 * inf) makes every slab of
 // ray_aabb_intersect NaN, so the reference's batch test (shader.comp:197-207) fails for every
@@ -448,7 +571,10 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
     if (GEOM == 2 && ray_misses_all_batches(o, d)) return;
     f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:336
     bool unused = false;
-    if (GEOM == 2) trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
+    if (GEOM == 2) {
+        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
+        else trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
+    }
     else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
 }
 
@@ -472,7 +598,10 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
     f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:377
     bool occluded = false;
     Hit unused;
-    if (GEOM == 2) trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+    if (GEOM == 2) {
+        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+        else trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+    }
     else walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     return occluded;
 }

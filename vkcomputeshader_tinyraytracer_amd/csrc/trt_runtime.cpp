@@ -25,6 +25,7 @@
 
 namespace trt {
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
+uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4);
 bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris);
 }
@@ -46,6 +47,7 @@ struct trt_ctx {
     BatchRec* d_batches = nullptr;
     float4* d_nodes = nullptr; // implicit 8-ary hierarchy over the batches
     trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
+    trt::Bvh4Node* d_bvh4 = nullptr; // the same, 4-wide
     TriGeo* d_bvh_tris = nullptr;
     uint32_t node_off[11] = {0};
     uint32_t top = 0;
@@ -106,6 +108,7 @@ void free_scene(trt_ctx* c) {
     (void)hipFree(c->d_batches);
     (void)hipFree(c->d_nodes);
     (void)hipFree(c->d_bvh);
+    (void)hipFree(c->d_bvh4);
     (void)hipFree(c->d_bvh_tris);
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade);
@@ -114,6 +117,7 @@ void free_scene(trt_ctx* c) {
     c->d_batches = nullptr;
     c->d_nodes = nullptr;
     c->d_bvh = nullptr;
+    c->d_bvh4 = nullptr;
     c->d_bvh_tris = nullptr;
     c->top = 0;
     c->d_geo = nullptr;
@@ -437,7 +441,12 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
     std::vector<trt::BvhNode> bvh;
     std::vector<TriGeo> bvh_tris;
     if (nmodel && trt::build_bvh(tris, ntri, models, nmodel, bvh, bvh_tris)) {
+        std::vector<trt::Bvh4Node> bvh4;
+        // the 4-wide walk only when its worst-case stack fits (else the BVH2 walk: <= depth)
+        if (trt::collapse_bvh4(bvh, bvh4) > (uint32_t)trt::kBvhStack) bvh4.clear();
         if ((rc = upload((void**)&c->d_bvh, bvh.data(), sizeof(trt::BvhNode) * bvh.size(), "upload bvh")) != TRT_OK ||
+            (!bvh4.empty() && (rc = upload((void**)&c->d_bvh4, bvh4.data(), sizeof(trt::Bvh4Node) * bvh4.size(),
+                                            "upload bvh4")) != TRT_OK) ||
             (rc = upload((void**)&c->d_bvh_tris, bvh_tris.data(), sizeof(TriGeo) * bvh_tris.size(),
                          "upload bvh triangles")) != TRT_OK) {
             free_scene(c);
@@ -508,6 +517,7 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.counters = c->d_counters;
     A.nodes = c->d_nodes;
     A.bvh = c->d_bvh;
+    A.bvh4 = c->d_bvh4;
     A.bvh_tris = c->d_bvh_tris;
     A.top = c->top;
     std::memcpy(A.node_off, c->node_off, sizeof(A.node_off));
