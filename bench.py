@@ -45,6 +45,8 @@ def parse():
                     help="frames in flight (trt_set_frames_in_flight; the reference's MAX_FRAMES_IN_FLIGHT = 2)")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (trt_set_subtree_split: 0 auto, 1 off)")
     ap.add_argument("--pmc", default=None, help="PMC summary json (tools/pmc_traffic.py) for roofline.traffic")
+    ap.add_argument("--tiled-frames", type=int, default=20,
+                    help="frames of the tiled-frame leg (C4 row-tiled over the ranks + RCCL gather); 0 skips it")
     return ap.parse_args()
 
 
@@ -95,6 +97,77 @@ def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
                   f"{med * 1e3:.1f} ms/frame; oracle/trt_oracle.c fast mode, -O3, rows over {threads} threads",
         "rays_match_gpu": bool(cpu_rays == rays_per_frame),
     }
+
+
+def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
+    """BASELINE configs[3]: ONE 3840x2160 C4 frame row-tiled across the ranks (interleaved
+    8-row bands, dist.TiledFrame) and gathered to rank 0 as RGBA8 over RCCL (xGMI), then
+    re-interleaved there.  Strong scaling: the frame is fixed, each rank renders 1/N of it.
+    A timed frame = band render + gather + re-interleave, bracketed like the main loop
+    (barrier + synchronize, max over ranks).  `frame_sha256` (rank 0's assembled frame) is the
+    same at every world size: the tiled frame is bit-identical to the 1-GPU frame."""
+    import hashlib
+
+    import torch
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+    from vkcomputeshader_tinyraytracer_amd import dist as D, scene as S
+
+    band = 8
+    sc = S.config_c4()
+    p = sc.params()
+    r = trt.Renderer(dev)
+    r.upload_scene(sc)
+    stream = torch.cuda.Stream()
+    r.set_stream(stream)
+    tf = D.TiledFrame(p.width, p.height, band_rows=band, device=torch.device("cuda", dev))
+    bp = D.band_params(p, band, world, rank)
+    _, _, st = r.draw_frame(bp, out8=tf.local, count=True)
+    torch.cuda.synchronize()
+    rays = st["primary_rays"] + st["secondary_rays"]
+
+    def frame():
+        r.draw_frame(bp, out8=tf.local)
+        with torch.cuda.stream(stream):  # the gather is ordered after the render on `stream`
+            return tf.render(lambda out: None)
+
+    for _ in range(3):
+        frame()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        img = frame()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, rays = float(mx[0].item()), int(t[1].item())
+    out = None
+    if rank == 0:
+        sha = hashlib.sha256(img.contiguous().cpu().numpy().tobytes()).hexdigest()
+        out = {
+            "workload": "C4: 3840x2160, 20 icospheres (102,400 tris), depth 4, one frame row-tiled "
+                        f"over {world} GPU(s) in interleaved {band}-row bands",
+            "scaling": "strong",
+            "collective": "dist.gather of padded RGBA8 band buffers to rank 0 (RCCL over xGMI)"
+                          if world > 1 else "none (1 GPU)",
+            "frames": frames,
+            "ms_per_frame": round(elapsed / frames * 1e3, 4),
+            "mray_s": round(rays * frames / elapsed / 1e6, 3),
+            "rays_per_frame": rays,
+            "gather_bytes_per_frame": int(tf.local.numel() * world) if world > 1 else 0,
+            "frame_sha256": sha,
+        }
+    r.close()
+    return out
 
 
 def main():
@@ -180,6 +253,7 @@ def main():
 
     value = total_rays * K / elapsed / 1e6
     ms_per_step = elapsed / K * 1e3
+    tiled = tiled_frame(args.tiled_frames, rank, world, dist, dev) if args.tiled_frames > 0 else None
 
     if rank == 0:
         achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
@@ -232,6 +306,8 @@ def main():
                         "physical HBM bytes per launch = traffic (PMC FETCH_SIZE + WRITE_SIZE)",
             },
         }
+        if tiled is not None:
+            result["tiled_frame"] = tiled
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(scene, params, rays_per_frame, args.cpu_seconds)
         print(json.dumps(result), flush=True)

@@ -47,6 +47,10 @@ for v in "$@"; do
             rm -f "$SRC/.prev_kernel.hip" ;;
         tpw4) variant tpw4 -DTRT_TPW=4 ;;
         w5prio) variant w5prio -DTRT_WAVES=5 -DTRT_PRIO=3 ;;
+        wpb2) variant wpb2 -DTRT_WPB=2 ;;
+        wpb4) variant wpb4 -DTRT_WPB=4 ;;
+        bgearly) variant bgearly -DTRT_BG_EARLY ;;
+        bgearly_wpb4) variant bgearly_wpb4 -DTRT_BG_EARLY -DTRT_WPB=4 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac
 done

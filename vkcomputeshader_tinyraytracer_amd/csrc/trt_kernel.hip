@@ -29,6 +29,22 @@
 
 namespace trt {
 
+// Waves per workgroup of the tile kernel (each wave traces its own 8x8 tile; no barriers).
+#ifndef TRT_WPB
+#define TRT_WPB 1
+#endif
+// Orders one wave's LDS accesses (the slab is private to the wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    if (TRT_WPB == 1) {
+        __syncthreads(); // one wave per workgroup
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+__device__ __forceinline__ uint32_t lane_id() { return TRT_WPB == 1 ? threadIdx.x : (threadIdx.x & 63u); }
+
 #define TRT_EPS 0.0001f /* MIN_EPSILON, shader.comp:78 */
 #define TRT_PI 3.14159265358979323846f /* PI, shader.comp:82 */
 #define TRT_GAMMA 2.2f /* GAMMA, shader.comp:81 */
@@ -214,14 +230,14 @@ __device__ __forceinline__ void walk_batches(const KArgs& A, f3 o, f3 d, f3 inv,
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
             for (int base = 0; base < count; base += 64) {
                 const int n = min(64, count - base);
-                __syncthreads(); // one wave per workgroup: orders the LDS reads of the previous slab
+                wave_lds_sync(); // orders the LDS reads of the previous slab
                 for (uint32_t i = rank; i < (uint32_t)n; i += nact) {
                     const float4* g = reinterpret_cast<const float4*>(A.geo + start + base + (int)i);
                     slab[i * 3u + 0u] = g[0];
                     slab[i * 3u + 1u] = g[1];
                     slab[i * 3u + 2u] = g[2];
                 }
-                __syncthreads();
+                wave_lds_sync();
                 if (hit) {
                     for (int k = 0; k < n; ++k) { // shader.comp:344-359 / 384-393
                         const float4 ga = slab[k * 3 + 0], gb = slab[k * 3 + 1], gc = slab[k * 3 + 2];
@@ -302,7 +318,7 @@ struct BvhStack {
     uint32_t priv[kBvhStack - kBvhLdsStack];
     int sp = 0;
     __device__ __forceinline__ explicit BvhStack(float4* slab)
-        : lds(reinterpret_cast<uint32_t*>(slab) + threadIdx.x) {}
+        : lds(reinterpret_cast<uint32_t*>(slab) + lane_id()) {}
     __device__ __forceinline__ void push(uint32_t v) {
         if (sp < kBvhLdsStack) lds[sp * 64] = v;
         else priv[sp - kBvhLdsStack] = v;
@@ -618,12 +634,18 @@ __device__ __forceinline__ float unorm8(uint32_t c) {
     return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
-__device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
-    if (!(A.flags & TRT_FLAG_ENVMAP)) return mk(0.2f, 0.7f, 0.8f); // BACKGROUND_COLOR :77
+// The four texels of a bilinear footprint and its weights: the gather is issued here and
+// consumed by env_blend, so a caller can place independent work between the two.
+struct EnvFetch {
+    uint32_t c00, c10, c01, c11;
+    float a, b;
+};
+
+__device__ __forceinline__ EnvFetch env_fetch(const KArgs& A, f3 d) {
 #ifdef TRT_DIAG_NO_ENV_FETCH
     {   // diagnostic: uv math without the texel gathers
         float u = (atan2f(d.z, d.x) + TRT_PI) / (2.0f * TRT_PI), v = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f)) / TRT_PI;
-        return mk(u, v, u * v);
+        return EnvFetch{0u, 0xffu, 0xff00u, 0xff0000u, u, v};
     }
 #endif
     float theta = atan2f(d.z, d.x);
@@ -649,18 +671,35 @@ __device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
     iy0 = min(max(iy0, 0), H - 1);
     const uint32_t* row0 = A.env + (size_t)iy0 * (size_t)W;
     const uint32_t* row1 = A.env + (size_t)iy1 * (size_t)W;
-    uint32_t c00 = row0[ix0], c10 = row0[ix1], c01 = row1[ix0], c11 = row1[ix1];
+    EnvFetch e;
+    e.c00 = row0[ix0];
+    e.c10 = row0[ix1];
+    e.c01 = row1[ix0];
+    e.c11 = row1[ix1];
+    e.a = a;
+    e.b = b;
+    return e;
+}
+
+// Bilinear blend of a fetched footprint (the second half of `background`).
+__device__ __forceinline__ f3 env_blend(const EnvFetch& e) {
+    const float a = e.a, b = e.b;
     float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b);
     float w01 = (1.0f - a) * b, w11 = a * b;
     float r[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int sh = 8 * k;
-        float t00 = unorm8((c00 >> sh) & 255u), t10 = unorm8((c10 >> sh) & 255u);
-        float t01 = unorm8((c01 >> sh) & 255u), t11 = unorm8((c11 >> sh) & 255u);
+        float t00 = unorm8((e.c00 >> sh) & 255u), t10 = unorm8((e.c10 >> sh) & 255u);
+        float t01 = unorm8((e.c01 >> sh) & 255u), t11 = unorm8((e.c11 >> sh) & 255u);
         r[k] = ((w00 * t00 + w10 * t10) + w01 * t01) + w11 * t11;
     }
     return mk(r[0], r[1], r[2]);
+}
+
+__device__ __forceinline__ f3 background(const KArgs& A, f3 d) {
+    if (!(A.flags & TRT_FLAG_ENVMAP)) return mk(0.2f, 0.7f, 0.8f); // BACKGROUND_COLOR :77
+    return env_blend(env_fetch(A, d));
 }
 
 // ---- cast_ray (shader.comp:423-583) --------------------------------------------------------
@@ -703,7 +742,7 @@ template <int CAP>
 struct DeferStack<CAP, true> {
     float* base; // this lane's column: base[(e * 8 + f) * 64]
     int n = 0;
-    __device__ __forceinline__ explicit DeferStack(float* lds) : base(lds + threadIdx.x) {}
+    __device__ __forceinline__ explicit DeferStack(float* lds) : base(lds + lane_id()) {}
     __device__ __forceinline__ void push(const Seg& x) {
         lds_put(base + n * 8 * 64, x);
         ++n;
@@ -729,7 +768,7 @@ struct HybridStack {
     float* base;
     Seg s[CP];
     int n = 0;
-    __device__ __forceinline__ explicit HybridStack(float* lds) : base(lds + threadIdx.x) {}
+    __device__ __forceinline__ explicit HybridStack(float* lds) : base(lds + lane_id()) {}
     __device__ __forceinline__ void push(const Seg& x) {
         if (n < CL) lds_put(base + n * 8 * 64, x);
         else s[n - CL] = x;
@@ -767,7 +806,7 @@ __device__ __forceinline__ void enqueue2(const KArgs& A, bool& sa, const Seg& a,
     const uint64_t act = __ballot(true);
     const int leader = __ffsll((unsigned long long)act) - 1;
     uint32_t base = 0;
-    if ((int)threadIdx.x == leader) base = atomicAdd(A.q_out_n, na + nb);
+    if ((int)lane_id() == leader) base = atomicAdd(A.q_out_n, na + nb);
     base = __shfl(base, leader, 64);
     const uint32_t ia = base + lane_rank(ba), ib = base + na + lane_rank(bb);
     auto put = [&](bool& f, uint32_t i, const Seg& x) {
@@ -815,10 +854,22 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
         scene_intersect<COUNT, GEOM>(A, cur.o, cur.d, h, cnt, slab);
         bool have_next = false;
         Seg next;
+#ifdef TRT_BG_EARLY
+        // Miss lanes issue their envmap gather before the hit lanes' shading and consume it
+        // after: the texel latency hides under the shading the wave executes meanwhile.  Each
+        // lane adds exactly one contribution per segment, so the sum order is unchanged.
+        const bool env_miss = h.kind == HIT_NONE && (A.flags & TRT_FLAG_ENVMAP);
+        EnvFetch ef;
+        if (env_miss) ef = env_fetch(A, cur.d);
+#endif
         if (h.kind == HIT_NONE) {
             if (COUNT) ++cnt.miss;
+#ifdef TRT_BG_EARLY
+            if (!env_miss) color = add(color, muls(mk(0.2f, 0.7f, 0.8f), cur.thr));
+#else
             f3 bg = background(A, cur.d);
             color = add(color, muls(bg, cur.thr));
+#endif
         } else {
             // Resolve the closest hit: point, normal, material (shader.comp:302-360).
             f3 p = add(cur.o, muls(cur.d, h.t));
@@ -931,6 +982,9 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 have_next = true;
             }
         }
+#ifdef TRT_BG_EARLY
+        if (env_miss) color = add(color, muls(env_blend(ef), cur.thr));
+#endif
         if (have_next) {
             cur = next;
         } else if (stk.n > 0) {
@@ -1031,7 +1085,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
 // colour in A.acc and is finished by finalize_spilled.
 template <int CAP, bool COUNT, int GEOM, bool SPLIT>
 __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = lane_id();
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
@@ -1125,15 +1179,31 @@ __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         unsigned long long w = wave_sum((unsigned long long)v[i]);
-        if (threadIdx.x == 0) atomicAdd(&A.counters[i], w);
+        if (lane_id() == 0) atomicAdd(&A.counters[i], w);
     }
 }
 
+template <int GEOM>
+constexpr int slab_float4s() { return GEOM == 1 ? 64 * 3 : GEOM == 2 ? (kBvhLdsStack > 0 ? kBvhLdsStack * 16 : 1) : 1; }
+
 template <int CAP, bool COUNT, int GEOM, bool SPLIT>
-__global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
+__global__ __launch_bounds__(64 * TRT_WPB, TRT_WAVES) void trace_kernel(KArgs A) {
+#if TRT_WPB > 1
+    // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
+    // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
+    __shared__ float lds_all[lds_stack_floats<CAP>() * TRT_WPB];
+    __shared__ float4 slab_all[slab_float4s<GEOM>() * TRT_WPB];
+    const uint32_t w = threadIdx.x >> 6;
+    float* lds = lds_all + w * lds_stack_floats<CAP>();
+    float4* slab = slab_all + w * slab_float4s<GEOM>();
+    const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
+    if (vb >= A.ntiles) return;
+#else
     __shared__ float lds[lds_stack_floats<CAP>()];
     // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
-    __shared__ float4 slab[GEOM == 1 ? 64 * 3 : GEOM == 2 ? (kBvhLdsStack > 0 ? kBvhLdsStack * 16 : 1) : 1];
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    const uint32_t vb = blockIdx.x;
+#endif
     Cnt cnt;
 #ifdef TRT_DIAG_WAVE_CLOCK
     // diagnostic: per-workgroup (tile | xcc << 28, start lo, duration, start hi) of the
@@ -1147,7 +1217,7 @@ __global__ __launch_bounds__(64, TRT_WAVES) void trace_kernel(KArgs A) {
         if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, b), cnt, lds, slab);
     }
 #else
-    trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, blockIdx.x), cnt, lds, slab);
+    trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, vb), cnt, lds, slab);
 #endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
@@ -1210,13 +1280,13 @@ __global__ __launch_bounds__(256) void finalize_spilled(KArgs A) {
 }
 
 template <int CAP, bool COUNT, int GEOM>
-static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid) {
+static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 block) {
     KArgs A = A0;
     const uint32_t D = A.max_depth, W = A.split_w;
     A.split_d1 = W;
     A.q_out = A.q_buf[0];
     A.q_out_n = &A.ctr->produced[0];
-    hipLaunchKernelGGL((trace_kernel<CAP, COUNT, GEOM, true>), grid, dim3(64), 0, stream, A);
+    hipLaunchKernelGGL((trace_kernel<CAP, COUNT, GEOM, true>), grid, block, 0, stream, A);
     uint32_t r = 1;
     for (uint32_t d0 = W; d0 < D && r <= kMaxSplitRounds; d0 += W, ++r) {
         A.split_d1 = d0 + W;
@@ -1240,6 +1310,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const uint32_t D = A.max_depth;
 #ifdef TRT_TPW
     const dim3 grid((A.ntiles + TRT_TPW - 1) / TRT_TPW), block(64);
+#elif TRT_WPB > 1
+    const dim3 grid(((A.ntiles + 8 * TRT_WPB - 1) / (8 * TRT_WPB)) * 8), block(64 * TRT_WPB);
 #else
     const dim3 grid(A.ntiles), block(64);
 #endif
@@ -1249,8 +1321,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
         if (e != hipSuccess) return e;
 #define TRT_SPLIT_G(CAP, G)                                                 \
     do {                                                                    \
-        if (count) launch_split<CAP, true, G>(A, stream, grid);            \
-        else launch_split<CAP, false, G>(A, stream, grid);                 \
+        if (count) launch_split<CAP, true, G>(A, stream, grid, block);            \
+        else launch_split<CAP, false, G>(A, stream, grid, block);                 \
     } while (0)
 #define TRT_SPLIT(CAP)                            \
     do {                                          \
