@@ -1014,13 +1014,15 @@ __device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
 
 __device__ __forceinline__ f3 primary_dir(const KArgs& A, uint32_t x, uint32_t y, uint32_t sample) {
     const uint32_t W = A.width, H = A.height;
-    const uint64_t pix = (uint64_t)y * W + x;
+    const uint32_t pix = y * W + x; // W, H <= 65536: fits
     f3 d;
     if (A.rays_in) {
-        const float* r = A.rays_in + 8 * pix; // Ray.dir (binding 1)
+        const float* r = A.rays_in + 8 * (size_t)pix; // Ray.dir (binding 1)
         d = mk(r[0], r[1], r[2]);
     } else {
-        const uint64_t row = (A.flags & TRT_FLAG_ROW_QUIRK) ? (pix + 1) / W : y;
+        // main.cpp:1501-1502 divides pix + 1 by W; with x + 1 <= W that is y + (x + 1 == W):
+        // the last column takes the next row's dy (App. B-1).  No 64-bit division per pixel.
+        const uint32_t row = ((A.flags & TRT_FLAG_ROW_QUIRK) && x + 1u == W) ? y + 1u : y;
         float dx, dy;
         if (A.spp <= 1) { // exact in float: half-integers (main.cpp:1501-1502)
             dx = ((float)x + 0.5f) - (float)W * 0.5f;
