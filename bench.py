@@ -100,11 +100,12 @@ def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
 
 
 def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
-    """BASELINE configs[3]: ONE 3840x2160 C4 frame row-tiled across the ranks (interleaved
+    """BASELINE configs[3]: a 3840x2160 C4 frame row-tiled across the ranks (interleaved
     8-row bands, dist.TiledFrame) and gathered to rank 0 as RGBA8 over RCCL (xGMI), then
     re-interleaved there.  Strong scaling: the frame is fixed, each rank renders 1/N of it.
-    A timed frame = band render + gather + re-interleave, bracketed like the main loop
-    (barrier + synchronize, max over ranks).  `frame_sha256` (rank 0's assembled frame) is the
+    Two frames in flight (dist.PipelinedTiles, main.cpp:45): frame i's gather overlaps frame
+    i+1's render.  The timed region (barrier + synchronize on both sides, max over ranks)
+    covers `frames` frames end to end.  `frame_sha256` (rank 0's last assembled frame) is the
     same at every world size: the tiled frame is bit-identical to the 1-GPU frame."""
     import hashlib
 
@@ -120,26 +121,24 @@ def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
     r.upload_scene(sc)
     stream = torch.cuda.Stream()
     r.set_stream(stream)
-    tf = D.TiledFrame(p.width, p.height, band_rows=band, device=torch.device("cuda", dev))
+    pipe = D.PipelinedTiles(p.width, p.height, band, torch.device("cuda", dev), stream)
     bp = D.band_params(p, band, world, rank)
-    _, _, st = r.draw_frame(bp, out8=tf.local, count=True)
+    _, _, st = r.draw_frame(bp, out8=pipe.tf[0].local, count=True)
     torch.cuda.synchronize()
     rays = st["primary_rays"] + st["secondary_rays"]
 
-    def frame():
-        r.draw_frame(bp, out8=tf.local)
-        with torch.cuda.stream(stream):  # the gather is ordered after the render on `stream`
-            return tf.render(lambda out: None)
+    def render(out):
+        r.draw_frame(bp, out8=out)
 
-    for _ in range(3):
-        frame()
+    for _ in range(4):
+        pipe.submit(render)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(frames):
-        img = frame()
+        img = pipe.submit(render)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -157,13 +156,15 @@ def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
             "workload": "C4: 3840x2160, 20 icospheres (102,400 tris), depth 4, one frame row-tiled "
                         f"over {world} GPU(s) in interleaved {band}-row bands",
             "scaling": "strong",
-            "collective": "dist.gather of padded RGBA8 band buffers to rank 0 (RCCL over xGMI)"
+            "collective": "dist.gather of padded RGBA8 band buffers to rank 0 (RCCL over xGMI), "
+                          "overlapped with the next frame's render (2 frames in flight)"
                           if world > 1 else "none (1 GPU)",
             "frames": frames,
             "ms_per_frame": round(elapsed / frames * 1e3, 4),
+            "frames_per_s": round(frames / elapsed, 3),
             "mray_s": round(rays * frames / elapsed / 1e6, 3),
             "rays_per_frame": rays,
-            "gather_bytes_per_frame": int(tf.local.numel() * world) if world > 1 else 0,
+            "gather_bytes_per_frame": int(pipe.tf[0].local.numel() * world) if world > 1 else 0,
             "frame_sha256": sha,
         }
     r.close()

@@ -112,3 +112,30 @@ def test_tiled_frame_two_processes():
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def test_pipelined_tiles_frames_in_flight(gpu_renderer):
+    """dist.PipelinedTiles (the bench's tiled-frame leg): with two frames in flight every
+    submitted frame (distinct cameras) comes out equal to the one-at-a-time render."""
+    torch = pytest.importorskip("torch")
+    sc = S.config_c3(160, 96, env_size=ENV)
+    gpu_renderer.upload_scene(sc)
+    p = sc.params()
+    stream = torch.cuda.Stream()
+    gpu_renderer.set_stream(stream)
+    ubos = [S.make_ubo(cam=(0.05 * i, 0.0, -0.1 * i)) for i in range(5)]
+    try:
+        pipe = D.PipelinedTiles(p.width, p.height, 8, torch.device("cuda", 0), stream)
+        got = []
+        for u in ubos:
+            gpu_renderer.update_ubo(u)
+            img = pipe.submit(lambda out: gpu_renderer.draw_frame(p, out8=out))
+            pipe.comm.synchronize()
+            got.append(img.cpu().numpy().copy())
+    finally:
+        gpu_renderer.set_stream(None)
+    for u, g in zip(ubos, got):
+        gpu_renderer.update_ubo(u)
+        one, _, _ = gpu_renderer.draw_frame(p)
+        assert np.array_equal(g, one)
+    gpu_renderer.update_ubo(sc.ubo)

@@ -8,7 +8,7 @@ mkdir -p "$LOG"
 export TMPDIR=/tmp
 cd /tmp
 CFG=${CFG:-C2}
-BENCH=("$ROOT/bench.py" --config "$CFG" --steps ${STEPS:-20} --warmup 2 --no-cpu ${BENCH_EXTRA:-})
+BENCH=("$ROOT/bench.py" --config "$CFG" --steps ${STEPS:-20} --warmup 2 --no-cpu --tiled-frames 0 ${BENCH_EXTRA:-})
 run() { # name counters...
     local name=$1
     shift

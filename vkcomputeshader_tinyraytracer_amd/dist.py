@@ -78,6 +78,42 @@ class TiledFrame:
         return self.frame
 
 
+class PipelinedTiles:
+    """Two TiledFrame buffers used alternately, so frame i's gather (on a communication
+    stream) overlaps frame i+1's band render (on the renderer's stream) — the tiled analogue
+    of the reference's two frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT = 2).  CUDA
+    (HIP) devices only: `render_fn(out)` must enqueue its render of `out` on `render_stream`.
+
+    submit() returns the frame tensor rank `dst` will hold once the communication stream has
+    run (None on the other ranks); that buffer is reused two submits later, so read it (on the
+    communication stream, or after synchronize()) before then."""
+
+    def __init__(self, width: int, height: int, band_rows: int, device: torch.device, render_stream,
+                 group=None, dst: int = 0):
+        self.tf = [TiledFrame(width, height, band_rows, group, dst, device) for _ in range(2)]
+        self.render_stream = render_stream
+        self.comm = torch.cuda.Stream(device)
+        self.rendered = [torch.cuda.Event(), torch.cuda.Event()]
+        self.gathered = [None, None]
+        self.i = 0
+
+    def submit(self, render_fn: Callable[[torch.Tensor], None]) -> torch.Tensor | None:
+        b = self.i % 2
+        tf = self.tf[b]
+        if self.gathered[b] is not None:  # the gather that last read this buffer is done
+            self.render_stream.wait_event(self.gathered[b])
+        render_fn(tf.local)
+        self.rendered[b].record(self.render_stream)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.rendered[b])
+            out = tf.render(lambda _: None)
+            ev = torch.cuda.Event()
+            ev.record(self.comm)
+            self.gathered[b] = ev
+        self.i += 1
+        return out
+
+
 def hip_render_fn(renderer, params: T.Params, band_rows: int, world: int, rank: int):
     """render_fn for TiledFrame backed by the HIP kernel (device output pointers)."""
     p = band_params(params, band_rows, world, rank)
