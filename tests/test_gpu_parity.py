@@ -306,3 +306,29 @@ def test_overlapping_batches_fall_back_to_walk(gpu_renderer):
     sc = S.Scene("overlap", S.make_ubo(), tris, models, S.cached_envmap(*SMALL_ENV), 80, 60, 5,
                  flags=T.FLAG_FLOOR | T.FLAG_ENVMAP | T.FLAG_ROW_QUIRK)
     _check(gpu_renderer, sc)
+
+
+def test_bvh_four_wave_build_bit_identical(gpu_renderer, golden_meshes, monkeypatch):
+    """The BVH walk compiled for 4 waves per SIMD (GEOM 3, picked for large meshes; forced here
+    with TRT_BVH_WAVES4, read at trt_create) renders exactly what the 3-wave build renders:
+    images, rayOut and every counter, with and without the subtree split."""
+    from vkcomputeshader_tinyraytracer_amd import Renderer
+
+    scenes = [S.config_c3(240, 136, env_size=SMALL_ENV),
+              S.config_reference_default(golden_meshes, env_size=SMALL_ENV, width=160, height=120)]
+    out = {}
+    for force in ("0", "1"):
+        monkeypatch.setenv("TRT_BVH_WAVES4", force)
+        with Renderer(0) as r:
+            for i, sc in enumerate(scenes):
+                r.upload_scene(sc)
+                out[force, i] = r.draw_frame(sc.params(), want32=True, count=True)
+                r.set_subtree_split(3)
+                out[force, i, "split"] = r.draw_frame(sc.params(), want32=True, count=True)
+                r.set_subtree_split(0)
+    monkeypatch.delenv("TRT_BVH_WAVES4")
+    for key in [k for k in out if k[0] == "0"]:
+        a8, a32, ast = out[key]
+        b8, b32, bst = out[("1",) + key[1:]]
+        assert np.array_equal(a8, b8) and np.array_equal(a32, b32), key
+        assert {k: v for k, v in ast.items() if k != "kernel_ms"} == {k: v for k, v in bst.items() if k != "kernel_ms"}

@@ -47,6 +47,9 @@ for v in "$@"; do
             rm -f "$SRC/.prev_kernel.hip" ;;
         tpw4) variant tpw4 -DTRT_TPW=4 ;;
         w5prio) variant w5prio -DTRT_WAVES=5 -DTRT_PRIO=3 ;;
+        w4) variant w4 -DTRT_WAVES=4 ;;
+        w4s16) variant w4s16 -DTRT_WAVES=4 -DTRT_BVH_LDS_N=16 ;;
+        s16) variant s16 -DTRT_BVH_LDS_N=16 ;;
         wpb2) variant wpb2 -DTRT_WPB=2 ;;
         wpb4) variant wpb4 -DTRT_WPB=4 ;;
         bgearly) variant bgearly -DTRT_BG_EARLY ;;

@@ -137,6 +137,7 @@ struct KArgs {
     uint32_t top;                     // levels above the batches: 8^top >= nbatch
     uint32_t ntx;                     // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
+    uint32_t bvh_waves4;          // BVH walk: the 4-waves-per-SIMD build (GEOM 3)
     // subtree split: this launch traces depths < split_d1; children at depth split_d1 become
     // tasks (split_d1 >= max_depth: no split).  split_w: the window (0 = split off).
     uint32_t split_w, split_d1;

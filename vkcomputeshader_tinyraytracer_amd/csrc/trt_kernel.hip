@@ -311,29 +311,38 @@ __device__ __forceinline__ bool bvh_box(f3 o, f3 inv, const float* lo, const flo
 #ifndef TRT_BVH_LDS
 #define TRT_BVH_LDS 1
 #endif
-constexpr int kBvhLdsStack = TRT_BVH_LDS ? 24 : 0;
+#ifndef TRT_BVH_LDS_N
+#define TRT_BVH_LDS_N 24
+#endif
+constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 
+// GEOM 3 is the BVH walk compiled for 4 waves per SIMD (<= 128 VGPRs) with a 16-entry LDS
+// stack, so 16 waves fit a CU's LDS (16 x (4 KB stack + 6 KB deferred segments) = 160 KB).
+template <int GEOM>
+constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? 16 : 0) : kBvhLdsStack; }
+
+template <int N>
 struct BvhStack {
     uint32_t* lds; // this lane's column
-    uint32_t priv[kBvhStack - kBvhLdsStack];
+    uint32_t priv[kBvhStack - N];
     int sp = 0;
     __device__ __forceinline__ explicit BvhStack(float4* slab)
         : lds(reinterpret_cast<uint32_t*>(slab) + lane_id()) {}
     __device__ __forceinline__ void push(uint32_t v) {
-        if (sp < kBvhLdsStack) lds[sp * 64] = v;
-        else priv[sp - kBvhLdsStack] = v;
+        if (sp < N) lds[sp * 64] = v;
+        else priv[sp - N] = v;
         ++sp;
     }
     __device__ __forceinline__ uint32_t pop() {
         --sp;
-        return sp < kBvhLdsStack ? lds[sp * 64] : priv[sp - kBvhLdsStack];
+        return sp < N ? lds[sp * 64] : priv[sp - N];
     }
 };
 
-template <bool COUNT, bool SHADOW>
+template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                           float max_dist, Cnt& c, float4* slab) {
-    BvhStack stack(slab);
+    BvhStack<bvh_lds_entries<GEOM>()> stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
 #ifdef TRT_DIAG_PIXEL_WORK
@@ -480,10 +489,10 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
 
 // 4-wide traversal: the four child boxes of a node in one 128-B fetch, entered nearest first
 // (the others pushed farthest first, so the next pop is the next nearest).
-template <bool COUNT, bool SHADOW>
+template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
-    BvhStack stack(slab);
+    BvhStack<bvh_lds_entries<GEOM>()> stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
     for (;;) {
@@ -584,12 +593,12 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return;
-    if (GEOM == 2 && ray_misses_all_batches(o, d)) return;
+    if (GEOM >= 2 && ray_misses_all_batches(o, d)) return;
     f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:336
     bool unused = false;
-    if (GEOM == 2) {
-        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
-        else trace_bvh<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
+    if (GEOM >= 2) {
+        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
+        else trace_bvh<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
     }
     else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
 }
@@ -610,13 +619,13 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return false;
-    if (GEOM == 2 && ray_misses_all_batches(o, d)) return false;
+    if (GEOM >= 2 && ray_misses_all_batches(o, d)) return false;
     f3 inv = mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:377
     bool occluded = false;
     Hit unused;
-    if (GEOM == 2) {
-        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
-        else trace_bvh<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+    if (GEOM >= 2) {
+        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+        else trace_bvh<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     }
     else walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     return occluded;
@@ -1186,10 +1195,14 @@ __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
 }
 
 template <int GEOM>
-constexpr int slab_float4s() { return GEOM == 1 ? 64 * 3 : GEOM == 2 ? (kBvhLdsStack > 0 ? kBvhLdsStack * 16 : 1) : 1; }
+constexpr int slab_float4s() {
+    return GEOM == 1 ? 64 * 3 : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
+}
+template <int GEOM>
+constexpr int waves_per_simd() { return GEOM == 3 ? 4 : TRT_WAVES; }
 
 template <int CAP, bool COUNT, int GEOM, bool SPLIT>
-__global__ __launch_bounds__(64 * TRT_WPB, TRT_WAVES) void trace_kernel(KArgs A) {
+__global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_kernel(KArgs A) {
 #if TRT_WPB > 1
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
     // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
@@ -1242,9 +1255,9 @@ __global__ __launch_bounds__(64 * TRT_WPB, TRT_WAVES) void trace_kernel(KArgs A)
 // window-edge children go to the next queue) and add the subtree's colour to its pixel's
 // fixed-point sum.  Every wave leaves once the queue is drained.
 template <int CAP, bool COUNT, int GEOM>
-__global__ __launch_bounds__(64, TRT_WAVES) void trace_tasks(KArgs A) {
+__global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
-    __shared__ float4 slab[GEOM == 1 ? 64 * 3 : GEOM == 2 ? (kBvhLdsStack > 0 ? kBvhLdsStack * 16 : 1) : 1];
+    __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = min(*A.q_in_n, A.q_cap);
     for (;;) {
@@ -1297,8 +1310,9 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
         A.q_in_head = &A.ctr->head[r - 1];
         A.q_out = A.q_buf[r & 1];
         A.q_out_n = &A.ctr->produced[r];
-        // persistent: 3 one-wave workgroups per SIMD (the mesh kernels' occupancy)
-        hipLaunchKernelGGL((trace_tasks<CAP, COUNT, GEOM>), dim3(A.num_cus * 12), dim3(64), 0, stream, A);
+        // persistent: 3 one-wave workgroups per SIMD (the mesh kernels' occupancy; 4 for GEOM 3)
+        hipLaunchKernelGGL((trace_tasks<CAP, COUNT, GEOM>), dim3(A.num_cus * (GEOM == 3 ? 16 : 12)), dim3(64), 0,
+                           stream, A);
     }
     hipLaunchKernelGGL(finalize_spilled, dim3(A.num_cus), dim3(256), 0, stream, A);
 }
@@ -1317,7 +1331,7 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
 #else
     const dim3 grid(A.ntiles), block(64);
 #endif
-    const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? 2 : 1;
+    const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
     if (A.split_w >= 2 && A.split_w <= 5 && A.split_w < D && A.spp <= 1 && A.acc && A.ctr) {
         hipError_t e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
         if (e != hipSuccess) return e;
@@ -1330,7 +1344,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     do {                                          \
         if (geom == 0) TRT_SPLIT_G(CAP, 0);       \
         else if (geom == 1) TRT_SPLIT_G(CAP, 1);  \
-        else TRT_SPLIT_G(CAP, 2);                 \
+        else if (geom == 2) TRT_SPLIT_G(CAP, 2);  \
+        else TRT_SPLIT_G(CAP, 3);                 \
     } while (0)
         switch (A.split_w) {
         case 2: TRT_SPLIT(1); break;
@@ -1351,7 +1366,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     do {                                         \
         if (geom == 0) TRT_LAUNCH_G(CAP, 0);     \
         else if (geom == 1) TRT_LAUNCH_G(CAP, 1); \
-        else TRT_LAUNCH_G(CAP, 2);               \
+        else if (geom == 2) TRT_LAUNCH_G(CAP, 2); \
+        else TRT_LAUNCH_G(CAP, 3);               \
     } while (0)
     if (D <= 1) TRT_LAUNCH(0);
     else if (D <= 2) TRT_LAUNCH(1);

@@ -68,6 +68,7 @@ struct trt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
     uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
+    int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     int subtree_split = TRT_SPLIT_AUTO;
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
@@ -227,6 +228,7 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = (uint32_t)prop.multiProcessorCount;
     c->stream = c->own_stream;
+    if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
     *out = c;
     return TRT_OK;
 }
@@ -523,6 +525,11 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     std::memcpy(A.node_off, c->node_off, sizeof(A.node_off));
     A.ntx = (A.width + 7u) / 8u;
     A.ntiles = A.ntx * ((A.rows + 7u) / 8u);
+    // The BVH walk at 4 waves per SIMD (GEOM 3: <= 128 VGPRs, 16-entry LDS stack) hides more of
+    // the node-fetch latency of large meshes but spills a few registers: measured -13 % on C4
+    // (1,600 batches), +1 % on C3 and the shipped frame (80 / 594 batches), so large scenes only
+    // (profiles/r01_ab_occupancy.log).
+    A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : (c->nbatch >= 1024u ? 1u : 0u);
 }
 
 // The subtree-split window of a frame: 0 = off.  Auto: scenes with meshes (whose deep
