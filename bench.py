@@ -103,8 +103,8 @@ def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
     """BASELINE configs[3]: a 3840x2160 C4 frame row-tiled across the ranks (interleaved
     8-row bands, dist.TiledFrame) and gathered to rank 0 as RGBA8 over RCCL (xGMI), then
     re-interleaved there.  Strong scaling: the frame is fixed, each rank renders 1/N of it.
-    Two frames in flight (dist.PipelinedTiles, main.cpp:45): frame i's gather overlaps frame
-    i+1's render.  The timed region (barrier + synchronize on both sides, max over ranks)
+    Two frames in flight (dist.PipelinedTiles, main.cpp:45): frame i's gather and render
+    overlap frame i+1's render.  The timed region (barrier + synchronize on both sides, max over ranks)
     covers `frames` frames end to end.  `frame_sha256` (rank 0's last assembled frame) is the
     same at every world size: the tiled frame is bit-identical to the 1-GPU frame."""
     import hashlib
@@ -119,15 +119,16 @@ def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
     p = sc.params()
     r = trt.Renderer(dev)
     r.upload_scene(sc)
-    stream = torch.cuda.Stream()
-    r.set_stream(stream)
-    pipe = D.PipelinedTiles(p.width, p.height, band, torch.device("cuda", dev), stream)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    r.set_stream(streams[0])
+    pipe = D.PipelinedTiles(p.width, p.height, band, torch.device("cuda", dev), streams)
     bp = D.band_params(p, band, world, rank)
     _, _, st = r.draw_frame(bp, out8=pipe.tf[0].local, count=True)
     torch.cuda.synchronize()
     rays = st["primary_rays"] + st["secondary_rays"]
 
-    def render(out):
+    def render(out, stream):  # frames alternate between two streams: consecutive renders overlap
+        r.set_stream(stream)
         r.draw_frame(bp, out8=out)
 
     for _ in range(4):
@@ -157,7 +158,7 @@ def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
                         f"over {world} GPU(s) in interleaved {band}-row bands",
             "scaling": "strong",
             "collective": "dist.gather of padded RGBA8 band buffers to rank 0 (RCCL over xGMI), "
-                          "overlapped with the next frame's render (2 frames in flight)"
+                          "overlapped with the next frame's render (2 frames in flight on 2 render streams)"
                           if world > 1 else "none (1 GPU)",
             "frames": frames,
             "ms_per_frame": round(elapsed / frames * 1e3, 4),

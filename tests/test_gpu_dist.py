@@ -121,15 +121,19 @@ def test_pipelined_tiles_frames_in_flight(gpu_renderer):
     sc = S.config_c3(160, 96, env_size=ENV)
     gpu_renderer.upload_scene(sc)
     p = sc.params()
-    stream = torch.cuda.Stream()
-    gpu_renderer.set_stream(stream)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     ubos = [S.make_ubo(cam=(0.05 * i, 0.0, -0.1 * i)) for i in range(5)]
+
+    def render(out, stream):
+        gpu_renderer.set_stream(stream)
+        gpu_renderer.draw_frame(p, out8=out)
+
     try:
-        pipe = D.PipelinedTiles(p.width, p.height, 8, torch.device("cuda", 0), stream)
+        pipe = D.PipelinedTiles(p.width, p.height, 8, torch.device("cuda", 0), streams)
         got = []
         for u in ubos:
             gpu_renderer.update_ubo(u)
-            img = pipe.submit(lambda out: gpu_renderer.draw_frame(p, out8=out))
+            img = pipe.submit(render)
             pipe.comm.synchronize()
             got.append(img.cpu().numpy().copy())
     finally:

@@ -50,6 +50,8 @@ for v in "$@"; do
         w4) variant w4 -DTRT_WAVES=4 ;;
         w4s16) variant w4s16 -DTRT_WAVES=4 -DTRT_BVH_LDS_N=16 ;;
         s16) variant s16 -DTRT_BVH_LDS_N=16 ;;
+        g5) variant g5 -DTRT_G3_WAVES=5 -DTRT_G3_LDS=8 ;;
+        g4s8) variant g4s8 -DTRT_G3_LDS=8 ;;
         wpb2) variant wpb2 -DTRT_WPB=2 ;;
         wpb4) variant wpb4 -DTRT_WPB=4 ;;
         bgearly) variant bgearly -DTRT_BG_EARLY ;;

@@ -318,8 +318,14 @@ constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 
 // GEOM 3 is the BVH walk compiled for 4 waves per SIMD (<= 128 VGPRs) with a 16-entry LDS
 // stack, so 16 waves fit a CU's LDS (16 x (4 KB stack + 6 KB deferred segments) = 160 KB).
+#ifndef TRT_G3_WAVES
+#define TRT_G3_WAVES 4
+#endif
+#ifndef TRT_G3_LDS
+#define TRT_G3_LDS 16
+#endif
 template <int GEOM>
-constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? 16 : 0) : kBvhLdsStack; }
+constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS : 0) : kBvhLdsStack; }
 
 template <int N>
 struct BvhStack {
@@ -1199,7 +1205,7 @@ constexpr int slab_float4s() {
     return GEOM == 1 ? 64 * 3 : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
 }
 template <int GEOM>
-constexpr int waves_per_simd() { return GEOM == 3 ? 4 : TRT_WAVES; }
+constexpr int waves_per_simd() { return GEOM == 3 ? TRT_G3_WAVES : TRT_WAVES; }
 
 template <int CAP, bool COUNT, int GEOM, bool SPLIT>
 __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_kernel(KArgs A) {
@@ -1311,7 +1317,7 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
         A.q_out = A.q_buf[r & 1];
         A.q_out_n = &A.ctr->produced[r];
         // persistent: 3 one-wave workgroups per SIMD (the mesh kernels' occupancy; 4 for GEOM 3)
-        hipLaunchKernelGGL((trace_tasks<CAP, COUNT, GEOM>), dim3(A.num_cus * (GEOM == 3 ? 16 : 12)), dim3(64), 0,
+        hipLaunchKernelGGL((trace_tasks<CAP, COUNT, GEOM>), dim3(A.num_cus * (GEOM == 3 ? 4 * TRT_G3_WAVES : 12)), dim3(64), 0,
                            stream, A);
     }
     hipLaunchKernelGGL(finalize_spilled, dim3(A.num_cus), dim3(256), 0, stream, A);

@@ -80,30 +80,37 @@ class TiledFrame:
 
 class PipelinedTiles:
     """Two TiledFrame buffers used alternately, so frame i's gather (on a communication
-    stream) overlaps frame i+1's band render (on the renderer's stream) — the tiled analogue
-    of the reference's two frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT = 2).  CUDA
-    (HIP) devices only: `render_fn(out)` must enqueue its render of `out` on `render_stream`.
+    stream) overlaps frame i+1's band render — the tiled analogue of the reference's two
+    frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT = 2).  With two render streams the
+    band renders of consecutive frames also overlap each other (frame i+1's tiles fill the
+    GPU while frame i's slowest tiles finish).  CUDA (HIP) devices only: `render_fn(out,
+    stream)` must enqueue its render of `out` on `stream`, and two of them must be able to run
+    at once (trt_render into device outputs is, unless the frame uses the subtree split, whose
+    scratch a context shares between its trt_render calls; trt_render_frames gives concurrent
+    split frames their own slots).
 
     submit() returns the frame tensor rank `dst` will hold once the communication stream has
     run (None on the other ranks); that buffer is reused two submits later, so read it (on the
     communication stream, or after synchronize()) before then."""
 
-    def __init__(self, width: int, height: int, band_rows: int, device: torch.device, render_stream,
+    def __init__(self, width: int, height: int, band_rows: int, device: torch.device, render_streams,
                  group=None, dst: int = 0):
         self.tf = [TiledFrame(width, height, band_rows, group, dst, device) for _ in range(2)]
-        self.render_stream = render_stream
+        rs = list(render_streams) if isinstance(render_streams, (list, tuple)) else [render_streams]
+        self.render_streams = [rs[0], rs[-1]]
         self.comm = torch.cuda.Stream(device)
         self.rendered = [torch.cuda.Event(), torch.cuda.Event()]
         self.gathered = [None, None]
         self.i = 0
 
-    def submit(self, render_fn: Callable[[torch.Tensor], None]) -> torch.Tensor | None:
+    def submit(self, render_fn: Callable[[torch.Tensor, object], None]) -> torch.Tensor | None:
         b = self.i % 2
         tf = self.tf[b]
+        rs = self.render_streams[b]
         if self.gathered[b] is not None:  # the gather that last read this buffer is done
-            self.render_stream.wait_event(self.gathered[b])
-        render_fn(tf.local)
-        self.rendered[b].record(self.render_stream)
+            rs.wait_event(self.gathered[b])
+        render_fn(tf.local, rs)
+        self.rendered[b].record(rs)
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(self.rendered[b])
             out = tf.render(lambda _: None)
