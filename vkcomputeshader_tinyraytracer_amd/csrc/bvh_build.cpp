@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -56,7 +57,22 @@ struct Prim {
     uint32_t tri, batch, ni;
 };
 
+// SAH knobs: cost of one node visit in triangle tests (the split pays ct * parent area) and the
+// leaf bounds.  Overridable for tuning (TRT_BVH_CT, TRT_BVH_LEAF_MIN, TRT_BVH_LEAF_MAX).
+struct SahParams {
+    float ct = 0.0f;
+    uint32_t leaf_min = kBvhLeafMin, leaf_max = kBvhLeafMax;
+    SahParams() {
+        if (const char* e = std::getenv("TRT_BVH_CT")) ct = std::strtof(e, nullptr);
+        if (const char* e = std::getenv("TRT_BVH_LEAF_MIN")) leaf_min = (uint32_t)std::strtoul(e, nullptr, 10);
+        if (const char* e = std::getenv("TRT_BVH_LEAF_MAX")) leaf_max = (uint32_t)std::strtoul(e, nullptr, 10);
+        leaf_max = std::min<uint32_t>(std::max<uint32_t>(leaf_max, 1u), 16u); // 4-bit leaf count field
+        leaf_min = std::min(std::max<uint32_t>(leaf_min, 1u), leaf_max);
+    }
+};
+
 struct Builder {
+    SahParams sp;
     std::vector<Prim> prims;
     std::vector<BvhNode> nodes;
     std::vector<uint32_t> order;
@@ -73,7 +89,7 @@ struct Builder {
         }
         out_box = bb;
         const uint32_t n = e - b;
-        if (n <= kBvhLeafMin) return make_leaf(b, e);
+        if (n <= sp.leaf_min) return make_leaf(b, e);
         const bool median_only = depth >= kBvhSahDepth; // bounds the depth: <= 32 + log2(n) levels
         // binned SAH over the widest centroid axis
         int axis = 0;
@@ -115,14 +131,14 @@ struct Builder {
                     nr += cnt[m];
                 }
                 if (!nl || !nr) continue;
-                const float cost = left.area() * nl + right.area() * nr;
+                const float cost = sp.ct * bb.area() + left.area() * nl + right.area() * nr;
                 if (cost < best) {
                     best = cost;
                     best_k = k;
                 }
             }
             const float leaf_cost = bb.area() * n;
-            if (n <= kBvhLeafMax && !(best < leaf_cost)) return make_leaf(b, e);
+            if (n <= sp.leaf_max && !(best < leaf_cost)) return make_leaf(b, e);
             if (best_k >= 0) {
                 auto it = std::partition(prims.begin() + b, prims.begin() + e,
                                          [&](const Prim& p) { return bin_of(p) <= best_k; });
@@ -151,7 +167,7 @@ struct Builder {
         return idx;
     }
 
-    uint32_t make_leaf(uint32_t b, uint32_t e) { // 1 <= e - b <= kBvhLeafMax
+    uint32_t make_leaf(uint32_t b, uint32_t e) { // 1 <= e - b <= sp.leaf_max <= 16
         const uint32_t start = (uint32_t)order.size();
         for (uint32_t i = b; i < e; ++i) order.push_back(i);
         return kBvhLeafBit | ((e - b - 1u) << kBvhCountShift) | start;
@@ -205,7 +221,7 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
         B.prims.push_back(p);
     }
     if (B.prims.empty()) return false;
-    B.nodes.reserve(2 * B.prims.size() / kBvhLeafMin + 2);
+    B.nodes.reserve(2 * B.prims.size() / B.sp.leaf_min + 2);
     Box root;
     const uint32_t r = B.build(0, (uint32_t)B.prims.size(), root, 0);
     if (r & kBvhLeafBit) { // single leaf: wrap it in a node with an empty second child

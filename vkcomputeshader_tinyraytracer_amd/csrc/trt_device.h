@@ -50,7 +50,7 @@ static_assert(sizeof(TriShade) == 48, "TriShade is 3 x dwordx4");
 constexpr uint32_t kBvhLeafBit = 0x80000000u;
 constexpr uint32_t kBvhCountShift = 27u;
 constexpr uint32_t kBvhFirstMask = (1u << kBvhCountShift) - 1u;
-constexpr uint32_t kBvhLeafMin = 4u, kBvhLeafMax = 8u;
+constexpr uint32_t kBvhLeafMin = 2u, kBvhLeafMax = 4u; // SAH sweep: profiles/r01_ab_sah.log
 constexpr int kBvhSahDepth = 32;  // below this depth only median splits
 constexpr int kBvhStack = 64;     // traversal stack >= max depth (32 + log2(2^27))
 struct alignas(16) BvhNode {
