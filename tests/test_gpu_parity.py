@@ -332,3 +332,48 @@ def test_bvh_four_wave_build_bit_identical(gpu_renderer, golden_meshes, monkeypa
         b8, b32, bst = out[("1",) + key[1:]]
         assert np.array_equal(a8, b8) and np.array_equal(a32, b32), key
         assert {k: v for k, v in ast.items() if k != "kernel_ms"} == {k: v for k, v in bst.items() if k != "kernel_ms"}
+
+
+def _cube():
+    pos = np.array([(x, y, z) for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)], np.float32)
+    quads = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    idx = np.array([t for a, b, c, d in quads for t in ((a, b, c), (a, c, d))], np.uint32)
+    return pos, idx
+
+
+def test_axis_aligned_rays_replay(gpu_renderer):
+    """Rays with exact-zero direction components (1/d = inf in the reference's slab test) through
+    an axis-aligned cube whose faces lie on the origin's planes and an icosphere, replayed
+    through binding 1: the BVH's culling (finite culling reciprocals, tests/DESIGN §4.5) must
+    keep every triangle the reference accepts.  Kernel vs oracle, counters exact."""
+    pos, idx = _cube()
+    ipos, iidx = S.icosphere(3)
+    b = S.SceneBuilder()
+    b.add_mesh(pos, idx, S.ICE_MAT, scale=(1.0, 1.0, 1.0), translation=(1.0, 1.0, -4.0), normal_interp=0)
+    b.add_mesh(ipos, iidx, S.GLASS_MESH_MAT, scale=(1.5, 1.5, 1.5), translation=(0.0, 0.0, -9.0), normal_interp=1)
+    tris, models = b.arrays()
+    b.close()
+    W, H = 48, 32
+    sc = S.Scene("axis", S.make_ubo(), tris, models, S.cached_envmap(*SMALL_ENV), W, H, 6,
+                 flags=T.FLAG_FLOOR | T.FLAG_ENVMAP | T.FLAG_SPHERES)
+    rng = np.random.default_rng(11)
+    rays = np.zeros(W * H, T.RAY)
+    comps = np.array([0.0, 0.0, 0.0, -0.0, 0.25, -0.25, 0.5, -0.125], np.float32)
+    for i in range(W * H):
+        d = np.array([rng.choice(comps), rng.choice(comps), -1.0], np.float32)
+        if i % 7 == 0:
+            d = np.array([0.0, 0.0, -1.0], np.float32)
+        elif i % 11 == 0:
+            d = np.array([0.0, -1.0, 0.0], np.float32)
+        d /= np.float32(np.sqrt(np.float32(d @ d)))
+        rays[i]["dir"] = (*d, 1.0)
+    p = sc.params()
+    gpu_renderer.upload_scene(sc)
+    g8, g32, gst = gpu_renderer.draw_frame(p, rays_in=rays, want32=True, count=True)
+    q = T.Params.from_buffer_copy(p)
+    q.rays_in = rays.ctypes.data
+    o8, o32, ost = orc.render(sc, q, want32=True)
+    assert _counts(gst) == _counts(ost), (gst, ost)
+    assert gst["tri_nearest"] > 0
+    assert_rgba8_close(g8, o8)
+    assert_float_close(g32, o32)
