@@ -503,37 +503,28 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
 #define TRT_BVH_WIDTH 4
 #endif
 
-// 4-wide traversal: the four child boxes of a node in one 128-B fetch, entered nearest first
-// (the others pushed farthest first, so the next pop is the next nearest).
-template <bool COUNT, bool SHADOW, int GEOM>
-__device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
-                                           float max_dist, Cnt& c, float4* slab) {
-    BvhStack<bvh_lds_entries<GEOM>()> stack(slab);
-    uint32_t node = 0;
-    float best = SHADOW ? max_dist : h.t;
-    for (;;) {
-        if (!(node & kBvhLeafBit)) {
-            const float4* p = reinterpret_cast<const float4*>(A.bvh4 + node);
-            const float4 lx = p[0], ly = p[1], lz = p[2], hx = p[3], hy = p[4], hz = p[5];
-            const uint4 ch = reinterpret_cast<const uint4*>(p)[6];
-#ifdef TRT_DIAG_PIXEL_WORK
-            ++c.wn;
-#endif
-            float t[4];
-            uint32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
-            const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
-            const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
-            int nh = 0;
+// One BVH4 node visit: the four child boxes tested against the ray, the entered children
+// sorted nearest first; the nearest becomes `node`, the others are pushed farthest first (so
+// the next pop is the next nearest).  Returns false when no child is entered.
+template <bool COUNT, typename Stack>
+__device__ __forceinline__ bool visit4(f3 o, f3 inv, float best, const float4& lx, const float4& ly,
+                                       const float4& lz, const float4& hx, const float4& hy, const float4& hz,
+                                       const uint4& ch, Stack& stack, uint32_t& node, Cnt& c) {
+    float t[4];
+    uint32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
+    const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
+    const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
+    int nh = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float tn;
-                const bool ok = r[i] != kBvh4None && bvh_box(o, inv, lo[i], hi[i], best, tn);
-                t[i] = ok ? tn : __builtin_huge_valf();
-                nh += ok ? 1 : 0;
-            }
-            if (COUNT) c.nt += (ch.x != kBvh4None) + (ch.y != kBvh4None) + (ch.z != kBvh4None) + (ch.w != kBvh4None);
-            if (nh > 0) {
-                // sorting network on (t, ref): ascending t, misses (t = inf) last
+    for (int i = 0; i < 4; ++i) {
+        float tn;
+        const bool ok = r[i] != kBvh4None && bvh_box(o, inv, lo[i], hi[i], best, tn);
+        t[i] = ok ? tn : __builtin_huge_valf();
+        nh += ok ? 1 : 0;
+    }
+    if (COUNT) c.nt += (ch.x != kBvh4None) + (ch.y != kBvh4None) + (ch.z != kBvh4None) + (ch.w != kBvh4None);
+    if (nh == 0) return false;
+    // sorting network on (t, ref): ascending t, misses (t = inf) last
 #define TRT_CSWAP(a, b)                                   \
     do {                                                  \
         const bool sw = t[b] < t[a];                      \
@@ -544,18 +535,62 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
         r[a] = sw ? rb : ra;                              \
         r[b] = sw ? ra : rb;                              \
     } while (0)
-                TRT_CSWAP(0, 1);
-                TRT_CSWAP(2, 3);
-                TRT_CSWAP(0, 2);
-                TRT_CSWAP(1, 3);
-                TRT_CSWAP(1, 2);
+    TRT_CSWAP(0, 1);
+    TRT_CSWAP(2, 3);
+    TRT_CSWAP(0, 2);
+    TRT_CSWAP(1, 3);
+    TRT_CSWAP(1, 2);
 #undef TRT_CSWAP
-                if (nh > 3) stack.push(r[3]);
-                if (nh > 2) stack.push(r[2]);
-                if (nh > 1) stack.push(r[1]);
-                node = r[0];
-                continue;
-            }
+    if (nh > 3) stack.push(r[3]);
+    if (nh > 2) stack.push(r[2]);
+    if (nh > 1) stack.push(r[1]);
+    node = r[0];
+    return true;
+}
+
+// 4-wide traversal: the four child boxes of a node in one 128-B fetch, entered nearest first.
+// The root is the same node for every lane: its record is read with wave-uniform (scalar)
+// loads, which the scalar cache serves, instead of a dependent per-lane vector fetch at the
+// start of every query.
+#ifndef TRT_ROOT_SCALAR
+#define TRT_ROOT_SCALAR 1
+#endif
+template <bool COUNT, bool SHADOW, int GEOM>
+__device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
+                                           float max_dist, Cnt& c, float4* slab) {
+    BvhStack<bvh_lds_entries<GEOM>()> stack(slab);
+    uint32_t node = 0;
+    float best = SHADOW ? max_dist : h.t;
+#if TRT_ROOT_SCALAR
+    {
+        // constant address space: the compiler may (and, the address being uniform, does) use
+        // scalar loads; the BVH is read-only for the whole launch
+        typedef __attribute__((address_space(4))) const float cfloat;
+        typedef __attribute__((address_space(4))) const uint32_t cuint;
+        const cfloat* R = (const cfloat*)(A.bvh4);
+        const cuint* RC = (const cuint*)(A.bvh4);
+#ifdef TRT_DIAG_PIXEL_WORK
+        ++c.wn;
+#endif
+        const float4 lx = make_float4(R[0], R[1], R[2], R[3]);
+        const float4 ly = make_float4(R[4], R[5], R[6], R[7]);
+        const float4 lz = make_float4(R[8], R[9], R[10], R[11]);
+        const float4 hx = make_float4(R[12], R[13], R[14], R[15]);
+        const float4 hy = make_float4(R[16], R[17], R[18], R[19]);
+        const float4 hz = make_float4(R[20], R[21], R[22], R[23]);
+        const uint4 ch = make_uint4(RC[24], RC[25], RC[26], RC[27]);
+        if (!visit4<COUNT>(o, inv, best, lx, ly, lz, hx, hy, hz, ch, stack, node, c)) return;
+    }
+#endif
+    for (;;) {
+        if (!(node & kBvhLeafBit)) {
+            const float4* p = reinterpret_cast<const float4*>(A.bvh4 + node);
+            const float4 lx = p[0], ly = p[1], lz = p[2], hx = p[3], hy = p[4], hz = p[5];
+            const uint4 ch = reinterpret_cast<const uint4*>(p)[6];
+#ifdef TRT_DIAG_PIXEL_WORK
+            ++c.wn;
+#endif
+            if (visit4<COUNT>(o, inv, best, lx, ly, lz, hx, hy, hz, ch, stack, node, c)) continue;
         } else if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
             occluded = true;
             return;
