@@ -51,6 +51,7 @@ for v in "$@"; do
         w4s16) variant w4s16 -DTRT_WAVES=4 -DTRT_BVH_LDS_N=16 ;;
         s16) variant s16 -DTRT_BVH_LDS_N=16 ;;
         noroot) variant noroot -DTRT_ROOT_SCALAR=0 ;;
+        noempty) variant noempty -DTRT_BVH4_EMPTY_BOX=0 ;;
         g5) variant g5 -DTRT_G3_WAVES=5 -DTRT_G3_LDS=8 ;;
         g4s8) variant g4s8 -DTRT_G3_LDS=8 ;;
         wpb2) variant wpb2 -DTRT_WPB=2 ;;

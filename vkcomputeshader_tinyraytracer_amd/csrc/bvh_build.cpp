@@ -327,8 +327,11 @@ uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4
                 }
                 nd.child[i] = r;
             } else {
-                nd.lox[i] = nd.loy[i] = nd.loz[i] = 0.0f;
-                nd.hix[i] = nd.hiy[i] = nd.hiz[i] = 0.0f;
+                // an empty slot: a point box at 1e30 on every axis, which no query can enter
+                // (its slab interval starts beyond any query's t bound of 1e10 or ends behind
+                // the origin), so the kernel tests all four slots without checking the ref
+                nd.lox[i] = nd.loy[i] = nd.loz[i] = kBvh4EmptyCoord;
+                nd.hix[i] = nd.hiy[i] = nd.hiz[i] = kBvh4EmptyCoord;
                 nd.child[i] = kBvh4None;
             }
             nd.pad[i] = 0;

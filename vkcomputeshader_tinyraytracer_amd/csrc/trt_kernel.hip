@@ -503,6 +503,9 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
 #define TRT_BVH_WIDTH 4
 #endif
 
+#ifndef TRT_BVH4_EMPTY_BOX
+#define TRT_BVH4_EMPTY_BOX 1
+#endif
 // One BVH4 node visit: the four child boxes tested against the ray, the entered children
 // sorted nearest first; the nearest becomes `node`, the others are pushed farthest first (so
 // the next pop is the next nearest).  Returns false when no child is entered.
@@ -518,7 +521,11 @@ __device__ __forceinline__ bool visit4(f3 o, f3 inv, float best, const float4& l
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float tn;
+#if TRT_BVH4_EMPTY_BOX
+        const bool ok = bvh_box(o, inv, lo[i], hi[i], best, tn); // unused slots hold a box no ray enters
+#else
         const bool ok = r[i] != kBvh4None && bvh_box(o, inv, lo[i], hi[i], best, tn);
+#endif
         t[i] = ok ? tn : __builtin_huge_valf();
         nh += ok ? 1 : 0;
     }
