@@ -442,7 +442,7 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
     }
 }
 
-// Tests the leaf `node` (1-8 triangles of the BVH-ordered array).  SHADOW: returns true when
+// Tests the leaf `node` (1-4 triangles of the BVH-ordered array).  SHADOW: returns true when
 // an accepted candidate occludes.  The next triangle's record is loaded before the current
 // one is tested (one exposed load latency per leaf instead of one per triangle).
 template <bool COUNT, bool SHADOW>
