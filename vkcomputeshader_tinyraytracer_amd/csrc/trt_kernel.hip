@@ -337,7 +337,10 @@ constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 template <int GEOM>
 constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS : 0) : kBvhLdsStack; }
 
-template <int N>
+// PUSH3: the branch-free push of up to three children (push_sorted) — used by the 3-wave
+// build: C3 -4 %, shipped frame -6 %; the 4-wave build (128-VGPR cap) is 3 % slower with it
+// (profiles/r01_ab_push3.log).
+template <int N, bool PUSH3 = false>
 struct BvhStack {
     uint32_t* lds; // this lane's column
     uint32_t priv[kBvhStack - N];
@@ -353,12 +356,29 @@ struct BvhStack {
         --sp;
         return sp < N ? lds[sp * 64] : priv[sp - N];
     }
+    // Pushes r[nh-1], ..., r[1] (r[1] ends on top), nh in 1..4.  While three more entries fit
+    // the LDS part, the three stores are unconditional: an unused one goes to slot sp + 3,
+    // above the new top.
+    __device__ __forceinline__ void push_sorted(const uint32_t (&r)[4], int nh) {
+        if (PUSH3 && sp + 3 < N) {
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                const int pos = k < nh ? sp + nh - 1 - k : sp + 3;
+                lds[pos * 64] = r[k];
+            }
+            sp += nh - 1;
+            return;
+        }
+        if (nh > 3) push(r[3]);
+        if (nh > 2) push(r[2]);
+        if (nh > 1) push(r[1]);
+    }
 };
 
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                           float max_dist, Cnt& c, float4* slab) {
-    BvhStack<bvh_lds_entries<GEOM>()> stack(slab);
+    BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2> stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
 #ifdef TRT_DIAG_PIXEL_WORK
@@ -548,9 +568,7 @@ __device__ __forceinline__ bool visit4(f3 o, f3 inv, float best, const float4& l
     TRT_CSWAP(1, 3);
     TRT_CSWAP(1, 2);
 #undef TRT_CSWAP
-    if (nh > 3) stack.push(r[3]);
-    if (nh > 2) stack.push(r[2]);
-    if (nh > 1) stack.push(r[1]);
+    stack.push_sorted(r, nh);
     node = r[0];
     return true;
 }
@@ -565,7 +583,7 @@ __device__ __forceinline__ bool visit4(f3 o, f3 inv, float best, const float4& l
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
-    BvhStack<bvh_lds_entries<GEOM>()> stack(slab);
+    BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2> stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
 #if TRT_ROOT_SCALAR
