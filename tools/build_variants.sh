@@ -48,6 +48,7 @@ for v in "$@"; do
         tpw4) variant tpw4 -DTRT_TPW=4 ;;
         w5prio) variant w5prio -DTRT_WAVES=5 -DTRT_PRIO=3 ;;
         w4) variant w4 -DTRT_WAVES=4 ;;
+        w6) variant w6 -DTRT_WAVES=6 ;;
         w4s16) variant w4s16 -DTRT_WAVES=4 -DTRT_BVH_LDS_N=16 ;;
         s16) variant s16 -DTRT_BVH_LDS_N=16 ;;
         noroot) variant noroot -DTRT_ROOT_SCALAR=0 ;;
