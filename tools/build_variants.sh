@@ -49,6 +49,7 @@ for v in "$@"; do
         w5prio) variant w5prio -DTRT_WAVES=5 -DTRT_PRIO=3 ;;
         w4) variant w4 -DTRT_WAVES=4 ;;
         w6) variant w6 -DTRT_WAVES=6 ;;
+        envpairs) variant envpairs -DTRT_ENV_PAIRS=1 ;;
         w4s16) variant w4s16 -DTRT_WAVES=4 -DTRT_BVH_LDS_N=16 ;;
         s16) variant s16 -DTRT_BVH_LDS_N=16 ;;
         noroot) variant noroot -DTRT_ROOT_SCALAR=0 ;;

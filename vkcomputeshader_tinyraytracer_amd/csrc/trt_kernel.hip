@@ -719,6 +719,9 @@ __device__ __forceinline__ float unorm8(uint32_t c) {
     return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
+#ifndef TRT_ENV_PAIRS
+#define TRT_ENV_PAIRS 1
+#endif
 // The four texels of a bilinear footprint and its weights: the gather is issued here and
 // consumed by env_blend, so a caller can place independent work between the two.
 struct EnvFetch {
@@ -754,13 +757,28 @@ __device__ __forceinline__ EnvFetch env_fetch(const KArgs& A, f3 d) {
     int iy1 = min(max(iy0 + 1, 0), H - 1);
     ix0 = min(max(ix0, 0), W - 1);
     iy0 = min(max(iy0, 0), H - 1);
-    const uint32_t* row0 = A.env + (size_t)iy0 * (size_t)W;
-    const uint32_t* row1 = A.env + (size_t)iy1 * (size_t)W;
     EnvFetch e;
-    e.c00 = row0[ix0];
-    e.c10 = row0[ix1];
-    e.c01 = row1[ix0];
-    e.c11 = row1[ix1];
+#if TRT_ENV_PAIRS
+    if (W >= 2) {
+        // Each row's two texels in one 8-byte load at base = min(ix0, W - 2): the footprint is
+        // (base, base + 1) except at the clamped edges, where ix0 / ix1 pick within the pair.
+        const int base = min(ix0, W - 2);
+        const uint2 p0 = *reinterpret_cast<const uint2*>(A.env + ((uint32_t)iy0 * (uint32_t)W + (uint32_t)base));
+        const uint2 p1 = *reinterpret_cast<const uint2*>(A.env + ((uint32_t)iy1 * (uint32_t)W + (uint32_t)base));
+        e.c00 = ix0 == base ? p0.x : p0.y;
+        e.c10 = ix1 == base ? p0.x : p0.y;
+        e.c01 = ix0 == base ? p1.x : p1.y;
+        e.c11 = ix1 == base ? p1.x : p1.y;
+    } else
+#endif
+    {
+        const uint32_t* row0 = A.env + (size_t)iy0 * (size_t)W;
+        const uint32_t* row1 = A.env + (size_t)iy1 * (size_t)W;
+        e.c00 = row0[ix0];
+        e.c10 = row0[ix1];
+        e.c01 = row1[ix0];
+        e.c11 = row1[ix1];
+    }
     e.a = a;
     e.b = b;
     return e;
