@@ -327,9 +327,9 @@ uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4
                 }
                 nd.child[i] = r;
             } else {
-                // an empty slot: a point box at 1e30 on every axis, which no query can enter
-                // (its slab interval starts beyond any query's t bound of 1e10 or ends behind
-                // the origin), so the kernel tests all four slots without checking the ref
+                // an empty slot: a box that is NaN on every axis, which no query can enter
+                // (trt_device.h kBvh4EmptyCoord), so the kernel tests all four slots without
+                // checking the ref
                 nd.lox[i] = nd.loy[i] = nd.loz[i] = kBvh4EmptyCoord;
                 nd.hix[i] = nd.hiy[i] = nd.hiz[i] = kBvh4EmptyCoord;
                 nd.child[i] = kBvh4None;

@@ -64,7 +64,9 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode is 64 B");
 // halving the dependent node fetches per query.  Child boxes SoA (lo_x[4] ...), 128 B = 8 x
 // dwordx4; an unused slot has child == kBvh4None.
 constexpr uint32_t kBvh4None = 0xFFFFFFFFu;
-constexpr float kBvh4EmptyCoord = 1e30f; // box of an unused slot (never entered)
+// Box of an unused slot: NaN on every axis.  Every slab product is then NaN, the NaN-ignoring
+// min/max give tnear = tfar = NaN, and `tnear <= tfar` fails for any ray and any distance bound.
+constexpr float kBvh4EmptyCoord = __builtin_nanf("");
 struct alignas(16) Bvh4Node {
     float lox[4], loy[4], loz[4];
     float hix[4], hiy[4], hiz[4];

@@ -542,7 +542,7 @@ __device__ __forceinline__ bool visit4(f3 o, f3 inv, float best, const float4& l
     for (int i = 0; i < 4; ++i) {
         float tn;
 #if TRT_BVH4_EMPTY_BOX
-        const bool ok = bvh_box(o, inv, lo[i], hi[i], best, tn); // unused slots hold a box no ray enters
+        const bool ok = bvh_box(o, inv, lo[i], hi[i], best, tn); // unused slots: an all-NaN box, never entered
 #else
         const bool ok = r[i] != kBvh4None && bvh_box(o, inv, lo[i], hi[i], best, tn);
 #endif
