@@ -377,3 +377,13 @@ def test_axis_aligned_rays_replay(gpu_renderer):
     assert gst["tri_nearest"] > 0
     assert_rgba8_close(g8, o8)
     assert_float_close(g32, o32)
+
+
+@pytest.mark.parametrize("far", [1e18, 1e25])
+def test_far_lights_mesh_scene(gpu_renderer, far):
+    """Lights so far away that shadow distance bounds are huge (1e18) or overflow to inf
+    (1e25: |L - p|^2 overflows): the BVH walk must neither enter unused node slots nor
+    fault, and the frame equals the oracle's (same overflow semantics)."""
+    sc = S.config_c3(96, 64, env_size=SMALL_ENV)
+    sc.ubo = S.make_ubo(lights=((far, far, far), (-far, far, 0.5 * far), (3.0, 50.0, -25.0)))
+    _check(gpu_renderer, sc)
