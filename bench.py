@@ -255,7 +255,12 @@ def main():
 
     value = total_rays * K / elapsed / 1e6
     ms_per_step = elapsed / K * 1e3
-    tiled = tiled_frame(args.tiled_frames, rank, world, dist, dev) if args.tiled_frames > 0 else None
+    tiled = None
+    if args.tiled_frames > 0:
+        try:
+            tiled = tiled_frame(args.tiled_frames, rank, world, dist, dev)
+        except Exception as e:  # the headline line is still printed; the failure is reported in it
+            tiled = {"error": f"{type(e).__name__}: {e}"} if rank == 0 else None
 
     if rank == 0:
         achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
