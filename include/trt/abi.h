@@ -184,6 +184,61 @@ uint32_t trt_output_rows(const trt_params* p);
  * TRT_FLAGS_REFERENCE. */
 void trt_params_default(trt_params* p);
 
+/* ---- multi-GPU frame tiling over RCCL (SURVEY §8(b) trt_render_multi, §8(e)) ----------
+ * Replaces the single-queue dispatch + submit (main.cpp:2108-2131, 2181-2205) with one frame
+ * row-tiled over the GPUs of a node: rows are dealt in interleaved bands of `band_rows` rows
+ * to ranks * groups_per_rank band groups (row y -> group (y / band_rows) % (ranks * groups);
+ * group g is rendered by rank g / groups_per_rank), every device renders its groups with the
+ * single-GPU kernel into compact RGBA8 buffers, one grouped ncclSend / ncclRecv moves them to
+ * the frame's root device over xGMI, and a re-interleave kernel assembles the frame there.
+ * The result is bit-identical to trt_render of the whole frame.  The scene is built once, on
+ * rank 0, and its device bindings are broadcast (ncclBroadcast) to the other devices.
+ * Output arrays `out_rgba8` have one entry per device of THIS process (trt_multi_local_count);
+ * only the root's entry is written (the others may be NULL). */
+typedef struct trt_multi trt_multi;
+
+#define TRT_MULTI_ID_BYTES 128 /* ncclUniqueId */
+#define TRT_ROOT_ROTATE (-1)   /* root of frame batch j = rank j % ranks (spreads the gathers'
+                                  ingest over every device's xGMI links) */
+
+/* One process drives `ndev` devices (ncclCommInitAll); rank i = devices[i]. */
+int trt_multi_create(trt_multi** out, const int* devices, uint32_t ndev);
+/* One process per GPU: every rank passes the same id (made by trt_multi_unique_id on one rank
+ * and exchanged out of band, e.g. MPI or torch.distributed), ncclCommInitRank. */
+int trt_multi_unique_id(uint8_t* id /* TRT_MULTI_ID_BYTES */);
+int trt_multi_create_rank(trt_multi** out, int hip_device, uint32_t nranks, uint32_t rank, const uint8_t* id);
+int trt_multi_destroy(trt_multi* m);
+const char* trt_multi_last_error(const trt_multi* m);
+uint32_t trt_multi_ranks(const trt_multi* m);       /* world size */
+uint32_t trt_multi_local_count(const trt_multi* m); /* devices driven by this process */
+/* The per-device context of local device i (its stream, split and frames-in-flight knobs). */
+trt_ctx* trt_multi_context(trt_multi* m, uint32_t local);
+/* Band groups per rank (default 1); more groups = finer interleave of the image over ranks. */
+int trt_multi_set_band_groups(trt_multi* m, uint32_t groups_per_rank);
+/* trt_upload_scene on rank 0 + broadcast of its device bindings; on the other ranks of a
+ * one-process-per-GPU run the arrays are ignored (may be NULL).  Collective. */
+int trt_multi_upload_scene(trt_multi* m, const trt_ubo* ubo, const trt_triangle* tris, uint32_t ntri,
+                           const trt_model* models, uint32_t nmodel, const uint8_t* env_rgba8,
+                           uint32_t env_w, uint32_t env_h);
+int trt_multi_update_ubo(trt_multi* m, const trt_ubo* ubo);
+/* One frame (p describes the whole frame; band_* must be 0) gathered on rank `root` (or
+ * TRT_ROOT_ROTATE).  out_rgba8[i]: width*height*4 bytes, a device pointer on local device i
+ * with TRT_FLAG_DEVICE_PTRS (then the call only enqueues on each context's stream), else a
+ * host pointer (synchronous).  TRT_FLAG_COUNT: st = counters summed over all ranks (a
+ * separate counting pass).  Collective. */
+int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int root,
+                     uint8_t* const* out_rgba8, trt_stats* st);
+/* The frame loop of trt_render_frames, tiled: frames i = 0..nframes-1 (UBO ubos[i], or the
+ * current one) in batches of `frames_per_gather` frames whose band buffers move in ONE grouped
+ * gather; frame i lands at out_rgba8[root's local index] + i * frame_stride.  Two batches are
+ * in flight: a batch's gather + re-interleave overlaps the next batch's render.  Requires
+ * TRT_FLAG_DEVICE_PTRS; only enqueues (complete on each context's stream).  Collective. */
+int trt_render_multi_frames(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
+                            uint32_t band_rows, int root, uint32_t frames_per_gather,
+                            uint8_t* const* out_rgba8, size_t frame_stride);
+/* Waits for every context stream of this process. */
+int trt_multi_synchronize(trt_multi* m);
+
 /* ---- host scene build (main.cpp:192-252, 1529-1580, 2290-2335) -------------------- */
 
 typedef struct trt_scene trt_scene;

@@ -45,6 +45,9 @@ def cases() -> dict:
     out["reference_default"] = (ref, ref.params())
     c5 = S.config_c4(W, H, env_size=ENV, spp=4)
     out["C4_spp4"] = (c5, c5.params())
+    # C5 (BASELINE configs[4]): the C4 scene at 16 PCG-jittered samples per pixel
+    c5_16 = S.config_c5(64, 48, env_size=ENV)
+    out["C5_spp16"] = (c5_16, c5_16.params())
     return out
 
 

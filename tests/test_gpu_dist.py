@@ -143,3 +143,85 @@ def test_pipelined_tiles_frames_in_flight(gpu_renderer):
         one, _, _ = gpu_renderer.draw_frame(p)
         assert np.array_equal(g, one)
     gpu_renderer.update_ubo(sc.ubo)
+
+
+def test_pipelined_tiles_deep_mesh_frame(gpu_renderer, golden_meshes):
+    """PipelinedTiles alternates trt_render between two streams; on a depth-20 mesh frame the
+    subtree split is active, so the two renders must not share task-queue scratch unfenced
+    (each stream gets its own split slot; a slot reused from another stream waits for it)."""
+    torch = pytest.importorskip("torch")
+    sc = S.config_reference_default(golden_meshes, env_size=ENV, width=160, height=120)
+    gpu_renderer.upload_scene(sc)
+    p = sc.params()
+    want, _, _ = gpu_renderer.draw_frame(p)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+
+    def render(out, stream):
+        gpu_renderer.set_stream(stream)
+        gpu_renderer.draw_frame(p, out8=out)
+
+    try:
+        pipe = D.PipelinedTiles(p.width, p.height, 8, torch.device("cuda", 0), streams)
+        got = []
+        for _ in range(6):
+            img = pipe.submit(render)
+            got.append(img)
+            if len(got) >= 2:  # the buffer of two submits ago is reused next: read it first
+                pipe.comm.synchronize()
+                got[-2] = got[-2].cpu().numpy().copy()
+        pipe.comm.synchronize()
+        got[-1] = got[-1].cpu().numpy().copy()
+    finally:
+        gpu_renderer.set_stream(None)
+    for g in got:
+        assert np.array_equal(g, want)
+
+
+def _nccl_worker(W, H, q):
+    import torch
+    import torch.distributed as dist
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        sc = S.config_c3(W, H, env_size=ENV)
+        r = trt.Renderer(0)
+        r.upload_scene(sc)
+        p = sc.params()
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+
+        def render(out, stream):
+            r.set_stream(stream)
+            r.draw_frame(p, out8=out)
+
+        pipe = D.PipelinedTiles(W, H, 8, torch.device("cuda", 0), streams)
+        assert pipe.tf[0].collective  # the gather runs through the process group
+        imgs = []
+        for _ in range(3):
+            img = pipe.submit(render)
+            pipe.comm.synchronize()
+            imgs.append(img.cpu().numpy().copy())
+        r.set_stream(None)
+        full, _, _ = r.draw_frame(p)
+        q.put(all(np.array_equal(i, full) for i in imgs))
+        r.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_tiles_nccl_world1():
+    """The RCCL ("nccl" backend) gather path of TiledFrame / PipelinedTiles executes at world
+    size 1 (the gather is not skipped when a process group exists)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_nccl_worker, args=(200, 120, q))
+    pr.start()
+    pr.join(240)
+    assert pr.exitcode == 0
+    assert q.get(timeout=5) is True

@@ -89,6 +89,15 @@ def test_jittered_spp(gpu_renderer, spp):
     _check(gpu_renderer, sc)
 
 
+def test_c5_sixteen_spp(gpu_renderer):
+    """C5 (BASELINE configs[4]): the ~100k-triangle C4 scene at 16 jittered samples per pixel,
+    reduced size; the per-pixel average of 16 clamped samples, then gamma."""
+    sc = S.config_c5(96, 64, env_size=SMALL_ENV)
+    assert sc.spp == 16
+    rep, st = _check(gpu_renderer, sc)
+    assert st["primary_rays"] == 96 * 64 * 16
+
+
 @pytest.mark.parametrize("flags", [
     0,
     T.FLAG_FLOOR,
@@ -386,4 +395,25 @@ def test_far_lights_mesh_scene(gpu_renderer, far):
     fault, and the frame equals the oracle's (same overflow semantics)."""
     sc = S.config_c3(96, 64, env_size=SMALL_ENV)
     sc.ubo = S.make_ubo(lights=((far, far, far), (-far, far, 0.5 * far), (3.0, 50.0, -25.0)))
+    _check(gpu_renderer, sc)
+
+
+def test_single_leaf_bvh_tests_each_triangle_once(gpu_renderer):
+    """A mesh small enough for one BVH leaf is wrapped in a root node whose second slot is
+    empty (an all-NaN box, never entered): every query entering the leaf tests its triangles
+    once, so the BVH's triangle-test count stays at the reference batch loop's (up to queries
+    that enter the leaf's padded box but not the batch box)."""
+    pos = np.array([[-2, -1, -10], [2, -1, -10], [2, 2, -10], [-2, 2, -10]], np.float32)
+    idx = np.array([[0, 1, 2], [0, 2, 3]], np.uint32)
+    b = S.SceneBuilder()
+    b.add_mesh(pos, idx, S.GLASS_MESH_MAT, normal_interp=0)
+    tris, models = b.arrays()
+    b.close()
+    sc = S.Scene("quad", S.make_ubo(), tris, models, None, 64, 48, 2, flags=T.FLAG_ROW_QUIRK)
+    gpu_renderer.upload_scene(sc)
+    _, _, bst = gpu_renderer.draw_frame(sc.params(), count=True)
+    pw = sc.params(flags=T.FLAG_ROW_QUIRK | T.FLAG_BATCH_WALK)
+    _, _, wst = gpu_renderer.draw_frame(pw, count=True)
+    assert wst["tri_tests"] > 0
+    assert bst["tri_tests"] <= wst["tri_tests"] * 1.05 + 8, (bst, wst)
     _check(gpu_renderer, sc)

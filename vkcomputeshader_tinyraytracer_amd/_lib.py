@@ -75,6 +75,22 @@ def lib() -> ctypes.CDLL:
         "trt_upload_envmap_jpeg": (c_int, [vp, vp, ctypes.c_size_t]),
         "trt_write_ppm": (c_int, [ctypes.c_char_p, vp, c_u32, c_u32]),
         "trt_write_png": (c_int, [ctypes.c_char_p, vp, c_u32, c_u32]),
+        "trt_multi_create": (c_int, [ctypes.POINTER(vp), ctypes.POINTER(c_int), c_u32]),
+        "trt_multi_unique_id": (c_int, [vp]),
+        "trt_multi_create_rank": (c_int, [ctypes.POINTER(vp), c_int, c_u32, c_u32, vp]),
+        "trt_multi_destroy": (c_int, [vp]),
+        "trt_multi_last_error": (ctypes.c_char_p, [vp]),
+        "trt_multi_ranks": (c_u32, [vp]),
+        "trt_multi_local_count": (c_u32, [vp]),
+        "trt_multi_context": (vp, [vp, c_u32]),
+        "trt_multi_set_band_groups": (c_int, [vp, c_u32]),
+        "trt_multi_upload_scene": (c_int, [vp, vp, vp, c_u32, vp, c_u32, vp, c_u32, c_u32]),
+        "trt_multi_update_ubo": (c_int, [vp, vp]),
+        "trt_render_multi": (c_int, [vp, ctypes.POINTER(Params), c_u32, c_int, ctypes.POINTER(vp),
+                                     ctypes.POINTER(Stats)]),
+        "trt_render_multi_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, c_u32, c_int, c_u32,
+                                            ctypes.POINTER(vp), ctypes.c_size_t]),
+        "trt_multi_synchronize": (c_int, [vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -122,4 +138,18 @@ ABI_SYMBOLS = (
     "trt_upload_envmap_jpeg",
     "trt_write_ppm",
     "trt_write_png",
+    "trt_multi_create",
+    "trt_multi_unique_id",
+    "trt_multi_create_rank",
+    "trt_multi_destroy",
+    "trt_multi_last_error",
+    "trt_multi_ranks",
+    "trt_multi_local_count",
+    "trt_multi_context",
+    "trt_multi_set_band_groups",
+    "trt_multi_upload_scene",
+    "trt_multi_update_ubo",
+    "trt_render_multi",
+    "trt_render_multi_frames",
+    "trt_multi_synchronize",
 )

@@ -229,11 +229,14 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
         for (int k = 0; k < 3; ++k) {
             nd.lo0[k] = root.lo[k];
             nd.hi0[k] = root.hi[k];
-            nd.lo1[k] = 1.0f;
-            nd.hi1[k] = -1.0f; // empty box: never entered
+            // NaN on every axis: every slab product is NaN, so tnear <= tfar fails for any ray
+            // (an inverted lo > hi box is not empty under NaN-ignoring min/max: it would act
+            // like the box between the two planes and test the leaf twice)
+            nd.lo1[k] = kBvh4EmptyCoord;
+            nd.hi1[k] = kBvh4EmptyCoord;
         }
         nd.child[0] = r;
-        nd.child[1] = r;
+        nd.child[1] = kBvh4None; // collapse_bvh4 keeps it an unused slot
         B.nodes.insert(B.nodes.begin(), nd);
     }
     nodes.swap(B.nodes);

@@ -1,0 +1,103 @@
+// trt_ctx.h — the context behind the C-ABI's opaque trt_ctx (internal to libtrt).
+//
+// Shared by trt_runtime.cpp (the single-GPU ABI) and trt_multi.cpp (the multi-GPU frame
+// tiling over RCCL, which broadcasts a context's scene bindings to the other devices).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/trt/abi.h"
+#include "trt_device.h"
+
+struct trt_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    trt_ubo ubo{};
+    bool have_scene = false;
+
+    trt::BatchRec* d_batches = nullptr;
+    float4* d_nodes = nullptr; // implicit 8-ary hierarchy over the batches
+    trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
+    trt::Bvh4Node* d_bvh4 = nullptr; // the same, 4-wide
+    trt::TriGeo* d_bvh_tris = nullptr;
+    uint32_t node_off[11] = {0};
+    uint32_t top = 0;
+    trt::TriGeo* d_geo = nullptr;
+    trt::TriShade* d_shade = nullptr;
+    trt::Mat* d_mats = nullptr;
+    uint32_t* d_env = nullptr;
+    uint32_t nbatch = 0, ntri = 0, nmat = 0, env_w = 0, env_h = 0;
+
+    void* d_out8 = nullptr;
+    size_t cap8 = 0;
+    void* d_out32 = nullptr;
+    size_t cap32 = 0;
+    void* d_rays = nullptr;
+    size_t caprays = 0;
+    unsigned long long* d_counters = nullptr;
+    uint32_t num_cus = 256;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
+    uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
+    int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
+    int subtree_split = TRT_SPLIT_AUTO;
+    // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
+    // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
+    // the counters.
+    struct SplitBufs {
+        trt::Task* q[2] = {nullptr, nullptr};
+        unsigned long long* acc = nullptr;
+        uint32_t* spilled = nullptr;
+        trt::SplitCtr* ctr = nullptr;
+        size_t npx = 0;  // pixels the buffers hold
+        uint32_t cap = 0; // tasks per queue
+        // The stream of the slot's last frame and an event after it: a frame on another
+        // stream waits for it before reusing the scratch (trt_render on alternating
+        // streams, e.g. dist.PipelinedTiles, must not race on the task queues).
+        hipStream_t last = nullptr;
+        hipEvent_t done = nullptr;
+    };
+    SplitBufs split[TRT_MAX_FRAMES_IN_FLIGHT];
+    hipStream_t render_slot_stream[TRT_MAX_FRAMES_IN_FLIGHT] = {}; // trt_render: stream -> slot (LRU)
+    uint32_t render_slot_next = 0;
+    std::vector<hipStream_t> aux; // frames-in-flight streams (frame i -> stream i % n)
+    std::vector<hipEvent_t> aux_ev;
+    hipEvent_t fork_ev = nullptr;
+    uint32_t fev_frames = 0;
+    // bytes of each scene binding on the device (trt::kSceneBuf* order), for the broadcast
+    size_t scene_bytes[9] = {0};
+};
+
+namespace trt {
+
+// The scene bindings of a context in a fixed order (the RCCL scene broadcast walks them).
+enum SceneBuf : int {
+    kSceneBatches = 0, kSceneNodes, kSceneBvh, kSceneBvh4, kSceneBvhTris, kSceneGeo, kSceneShade,
+    kSceneMats, kSceneEnv, kSceneBufs
+};
+void** scene_buf(trt_ctx* c, int k);
+
+// Everything besides the device buffers that trt_upload_scene derives (fixed size, broadcast
+// as bytes from the root device to the others).
+struct SceneHeader {
+    uint32_t magic;
+    uint32_t nbatch, ntri, nmat, env_w, env_h, top, pad;
+    uint32_t node_off[11];
+    uint32_t pad2;
+    uint64_t bytes[kSceneBufs];
+    trt_ubo ubo;
+};
+constexpr uint32_t kSceneMagic = 0x54525453u; // "STRT"
+
+// Fills h from a context with an uploaded scene.
+void scene_header(const trt_ctx* c, SceneHeader& h);
+// Drops c's scene and allocates empty device buffers of h's sizes (filled by the caller,
+// e.g. by ncclBroadcast), then adopts h's scalars.  Returns TRT_OK or an error code.
+int scene_adopt(trt_ctx* c, const SceneHeader& h);
+
+} // namespace trt

@@ -1476,3 +1476,40 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
 }
 
 } // namespace trt
+
+// ---- multi-GPU frame assembly (trt_multi.cpp) ----------------------------------------------
+//
+// Re-interleaves the compact band-group buffers a gather delivered to the root: output row y
+// of frame f belongs to band b = y / B, band group g = b % NG, compact row k = (b / NG) * B +
+// y % B (the inverse of band_row above), stored at gather + ((f * NG + g) * max_rows + k) * W.
+// One 256-thread workgroup per output row; rows are copied as 16-byte vectors when aligned.
+namespace trt {
+
+__global__ __launch_bounds__(256) void interleave_kernel(const uint32_t* __restrict__ gather, uint32_t* __restrict__ out,
+                                                         uint32_t W, uint32_t H, uint32_t B, uint32_t NG,
+                                                         uint32_t max_rows, size_t stride_px, int vec4) {
+    const uint32_t f = blockIdx.x / H, y = blockIdx.x % H;
+    const uint32_t b = y / B, g = b % NG, k = (b / NG) * B + y % B;
+    const uint32_t* src = gather + ((size_t)(f * NG + g) * max_rows + k) * W;
+    uint32_t* dst = out + (size_t)f * stride_px + (size_t)y * W;
+    if (vec4) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t i = threadIdx.x; i < W / 4u; i += blockDim.x) d4[i] = s4[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
+hipError_t launch_interleave(const uint32_t* gather, uint32_t* out, uint32_t width, uint32_t height,
+                             uint32_t band_rows, uint32_t groups, uint32_t max_rows, uint32_t nframes,
+                             size_t frame_stride_px, hipStream_t stream) {
+    if (!width || !height || !nframes) return hipSuccess;
+    const int vec4 = (width % 4u == 0u) && ((reinterpret_cast<uintptr_t>(out) & 15u) == 0u) &&
+                     (frame_stride_px % 4u == 0u) && ((reinterpret_cast<uintptr_t>(gather) & 15u) == 0u);
+    hipLaunchKernelGGL(interleave_kernel, dim3(height * nframes), dim3(256), 0, stream, gather, out, width, height,
+                       band_rows, groups, max_rows, frame_stride_px, vec4);
+    return hipGetLastError();
+}
+
+} // namespace trt

@@ -21,6 +21,7 @@
 
 #include "../../include/trt/abi.h"
 #include "jpeg.h"
+#include "trt_ctx.h"
 #include "trt_device.h"
 
 namespace trt {
@@ -36,57 +37,6 @@ using trt::Mat;
 using trt::TriGeo;
 using trt::TriShade;
 
-struct trt_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-    trt_ubo ubo{};
-    bool have_scene = false;
-
-    BatchRec* d_batches = nullptr;
-    float4* d_nodes = nullptr; // implicit 8-ary hierarchy over the batches
-    trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
-    trt::Bvh4Node* d_bvh4 = nullptr; // the same, 4-wide
-    TriGeo* d_bvh_tris = nullptr;
-    uint32_t node_off[11] = {0};
-    uint32_t top = 0;
-    TriGeo* d_geo = nullptr;
-    TriShade* d_shade = nullptr;
-    Mat* d_mats = nullptr;
-    uint32_t* d_env = nullptr;
-    uint32_t nbatch = 0, ntri = 0, nmat = 0, env_w = 0, env_h = 0;
-
-    void* d_out8 = nullptr;
-    size_t cap8 = 0;
-    void* d_out32 = nullptr;
-    size_t cap32 = 0;
-    void* d_rays = nullptr;
-    size_t caprays = 0;
-    unsigned long long* d_counters = nullptr;
-    uint32_t num_cus = 256;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
-    uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
-    int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
-    int subtree_split = TRT_SPLIT_AUTO;
-    // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
-    // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
-    // the counters.
-    struct SplitBufs {
-        trt::Task* q[2] = {nullptr, nullptr};
-        unsigned long long* acc = nullptr;
-        uint32_t* spilled = nullptr;
-        trt::SplitCtr* ctr = nullptr;
-        size_t npx = 0;  // pixels the buffers hold
-        uint32_t cap = 0; // tasks per queue
-    };
-    SplitBufs split[TRT_MAX_FRAMES_IN_FLIGHT];
-    std::vector<hipStream_t> aux; // frames-in-flight streams (frame i -> stream i % n)
-    std::vector<hipEvent_t> aux_ev;
-    hipEvent_t fork_ev = nullptr;
-    uint32_t fev_frames = 0;
-};
 
 namespace {
 
@@ -126,6 +76,7 @@ void free_scene(trt_ctx* c) {
     c->d_mats = nullptr;
     c->d_env = nullptr;
     c->nbatch = c->ntri = c->nmat = c->env_w = c->env_h = 0;
+    std::memset(c->scene_bytes, 0, sizeof(c->scene_bytes));
     c->have_scene = false;
 }
 
@@ -250,6 +201,7 @@ int trt_destroy(trt_ctx* c) {
         (void)hipFree(b.acc);
         (void)hipFree(b.spilled);
         (void)hipFree(b.ctr);
+        if (b.done) (void)hipEventDestroy(b.done);
     }
     for (hipStream_t s : c->aux) {
         (void)hipStreamSynchronize(s);
@@ -442,10 +394,12 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
     }
     std::vector<trt::BvhNode> bvh;
     std::vector<TriGeo> bvh_tris;
+    size_t bvh4_n = 0;
     if (nmodel && trt::build_bvh(tris, ntri, models, nmodel, bvh, bvh_tris)) {
         std::vector<trt::Bvh4Node> bvh4;
         // the 4-wide walk only when its worst-case stack fits (else the BVH2 walk: <= depth)
         if (trt::collapse_bvh4(bvh, bvh4) > (uint32_t)trt::kBvhStack) bvh4.clear();
+        bvh4_n = bvh4.size();
         if ((rc = upload((void**)&c->d_bvh, bvh.data(), sizeof(trt::BvhNode) * bvh.size(), "upload bvh")) != TRT_OK ||
             (!bvh4.empty() && (rc = upload((void**)&c->d_bvh4, bvh4.data(), sizeof(trt::Bvh4Node) * bvh4.size(),
                                             "upload bvh4")) != TRT_OK) ||
@@ -463,6 +417,19 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         c->env_w = env_w;
         c->env_h = env_h;
     }
+    size_t* sb = c->scene_bytes;
+    std::memset(sb, 0, sizeof(c->scene_bytes));
+    sb[trt::kSceneBatches] = std::max<size_t>(sizeof(BatchRec) * nmodel, 16);
+    sb[trt::kSceneNodes] = std::max<size_t>(sizeof(float4) * nodes.size(), 16);
+    sb[trt::kSceneGeo] = std::max<size_t>(sizeof(TriGeo) * ntri, 16);
+    sb[trt::kSceneShade] = std::max<size_t>(sizeof(TriShade) * ntri, 16);
+    sb[trt::kSceneMats] = sizeof(Mat) * mats.size();
+    if (c->d_bvh) {
+        sb[trt::kSceneBvh] = sizeof(trt::BvhNode) * bvh.size();
+        sb[trt::kSceneBvhTris] = sizeof(TriGeo) * bvh_tris.size();
+    }
+    if (c->d_bvh4) sb[trt::kSceneBvh4] = sizeof(trt::Bvh4Node) * bvh4_n;
+    if (c->d_env) sb[trt::kSceneEnv] = (size_t)env_w * env_h * 4;
     c->nbatch = nmodel;
     c->top = top;
     std::memcpy(c->node_off, node_off, sizeof(node_off));
@@ -550,13 +517,15 @@ uint32_t split_window(const trt_ctx* c, const trt_params* p) {
     return w < D ? w : 0u;
 }
 
-// Allocates slot `slot`'s split scratch for this frame size and fills A's split fields.
-int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
+// Allocates slot `slot`'s split scratch for this frame size and fills A's split fields; a
+// frame on `stream` waits for the slot's previous frame when that ran on another stream.
+int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipStream_t stream) {
     A.split_w = split_window(c, p);
     A.split_d1 = A.max_depth;
     A.num_cus = c->num_cus;
     if (!A.split_w) return TRT_OK;
     auto& b = c->split[slot];
+    if (b.last && b.last != stream) HIP_TRY(c, hipStreamWaitEvent(stream, b.done, 0));
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     if (npx > b.npx) {
         // queue capacity: 4 tasks per pixel per window edge (a full queue is not an error: the
@@ -591,6 +560,27 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     A.spilled = b.spilled;
     A.ctr = b.ctr;
     return TRT_OK;
+}
+
+// After a split frame's launches on `stream`: the slot's fence.
+int fence_split(trt_ctx* c, const KArgs& A, uint32_t slot, hipStream_t stream) {
+    if (!A.split_w) return TRT_OK;
+    auto& b = c->split[slot];
+    if (!b.done) HIP_TRY(c, hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(b.done, stream));
+    b.last = stream;
+    return TRT_OK;
+}
+
+// trt_render's split slot: one per distinct stream among the last TRT_MAX_FRAMES_IN_FLIGHT
+// (so renders alternating between streams overlap), reused least recently first.
+uint32_t render_slot(trt_ctx* c, hipStream_t s) {
+    for (uint32_t k = 0; k < TRT_MAX_FRAMES_IN_FLIGHT; ++k)
+        if (c->render_slot_stream[k] == s) return k;
+    const uint32_t k = c->render_slot_next;
+    c->render_slot_next = (k + 1) % TRT_MAX_FRAMES_IN_FLIGHT;
+    c->render_slot_stream[k] = s;
+    return k;
 }
 
 } // namespace
@@ -647,12 +637,13 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
             fill_ubo_args(A, c->ubo);
         }
         hipStream_t st = sv[i % nfl];
-        if ((rc = prepare_split(c, p, A, i % nfl)) != TRT_OK) return rc;
+        if ((rc = prepare_split(c, p, A, i % nfl, st)) != TRT_OK) return rc;
         A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
         const bool timed = timing && i % every == 0;
         const size_t k = 2 * (size_t)(i / every);
         if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], st));
         HIP_TRY(c, trt::launch_trace(A, st, false));
+        if ((rc = fence_split(c, A, i % nfl, st)) != TRT_OK) return rc;
         if (timed) {
             HIP_TRY(c, hipEventRecord(c->fev[k + 1], st));
             c->fev_frames = i / every + 1;
@@ -719,10 +710,12 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
             A.out32 = reinterpret_cast<float*>(c->d_out32);
         }
     }
-    if ((rc = prepare_split(c, p, A, 0)) != TRT_OK) return rc;
+    const uint32_t slot = render_slot(c, c->stream);
+    if ((rc = prepare_split(c, p, A, slot, c->stream)) != TRT_OK) return rc;
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
+    if ((rc = fence_split(c, A, slot, c->stream)) != TRT_OK) return rc;
     if (timing) HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
     if (out8 && !dev)
         HIP_TRY(c, hipMemcpyAsync(out8, c->d_out8, npx * 4, hipMemcpyDeviceToHost, c->stream));
@@ -809,6 +802,68 @@ extern "C" int trt_upload_envmap_jpeg(trt_ctx* c, const uint8_t* data, size_t le
     c->d_env = d;
     c->env_w = (uint32_t)im->width;
     c->env_h = (uint32_t)im->height;
+    c->scene_bytes[trt::kSceneEnv] = (size_t)im->width * im->height * 4;
     trt_jpeg_destroy(j);
     return TRT_OK;
 }
+
+// ---- scene export / adoption (the RCCL scene broadcast of trt_multi.cpp) --------------------
+
+namespace trt {
+
+void** scene_buf(trt_ctx* c, int k) {
+    switch (k) {
+    case kSceneBatches: return reinterpret_cast<void**>(&c->d_batches);
+    case kSceneNodes: return reinterpret_cast<void**>(&c->d_nodes);
+    case kSceneBvh: return reinterpret_cast<void**>(&c->d_bvh);
+    case kSceneBvh4: return reinterpret_cast<void**>(&c->d_bvh4);
+    case kSceneBvhTris: return reinterpret_cast<void**>(&c->d_bvh_tris);
+    case kSceneGeo: return reinterpret_cast<void**>(&c->d_geo);
+    case kSceneShade: return reinterpret_cast<void**>(&c->d_shade);
+    case kSceneMats: return reinterpret_cast<void**>(&c->d_mats);
+    default: return reinterpret_cast<void**>(&c->d_env);
+    }
+}
+
+void scene_header(const trt_ctx* c, SceneHeader& h) {
+    std::memset(&h, 0, sizeof(h));
+    h.magic = kSceneMagic;
+    h.nbatch = c->nbatch;
+    h.ntri = c->ntri;
+    h.nmat = c->nmat;
+    h.env_w = c->env_w;
+    h.env_h = c->env_h;
+    h.top = c->top;
+    std::memcpy(h.node_off, c->node_off, sizeof(h.node_off));
+    for (int k = 0; k < kSceneBufs; ++k) h.bytes[k] = c->scene_bytes[k];
+    h.ubo = c->ubo;
+}
+
+int scene_adopt(trt_ctx* c, const SceneHeader& h) {
+    if (h.magic != kSceneMagic) return fail(c, TRT_ERR_INVALID, "scene broadcast: bad header");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    free_scene(c);
+    for (int k = 0; k < kSceneBufs; ++k) {
+        if (!h.bytes[k]) continue;
+        void** p = scene_buf(c, k);
+        hipError_t e = hipMalloc(p, h.bytes[k]);
+        if (e != hipSuccess) {
+            free_scene(c);
+            return hip_fail(c, e, "scene broadcast: alloc");
+        }
+        c->scene_bytes[k] = h.bytes[k];
+    }
+    c->nbatch = h.nbatch;
+    c->ntri = h.ntri;
+    c->nmat = h.nmat;
+    c->env_w = h.env_w;
+    c->env_h = h.env_h;
+    c->top = h.top;
+    std::memcpy(c->node_off, h.node_off, sizeof(c->node_off));
+    c->ubo = h.ubo;
+    c->have_scene = true;
+    return TRT_OK;
+}
+
+} // namespace trt

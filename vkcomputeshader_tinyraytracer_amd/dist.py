@@ -43,8 +43,11 @@ class TiledFrame:
 
     def __init__(self, width: int, height: int, band_rows: int = 8, group=None, dst: int = 0,
                  device: torch.device | None = None):
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # with a process group the gather always runs, even at world size 1 (then it is the
+        # backend's local copy), so the collective path is the one exercised at every N
+        self.collective = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.collective else 1
+        self.rank = dist.get_rank(group) if self.collective else 0
         self.group, self.dst = group, dst
         self.width, self.height, self.band_rows = width, height, band_rows
         self.device = device if device is not None else torch.device("cpu")
@@ -66,7 +69,7 @@ class TiledFrame:
         """`render_fn(out)` renders this rank's compact bands into out[:len(my_rows)].  Returns
         the full (H, W, 4) frame on `dst`, None elsewhere."""
         render_fn(self.local)
-        if self.world == 1:
+        if not self.collective:
             return self.local[: self.height]
         dist.gather(self.local, self.gathered, dst=self.dst, group=self.group)
         if self.rank != self.dst:
