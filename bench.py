@@ -1,24 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path: Mray/s (primary + secondary) at 1024x768, depth 4 (BASELINE.json).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|ref|readme] [--no-cpu]
 
-One step = one frame of the configuration rendered by the HIP kernel through the C-ABI
-(trt_render, device output pointers, inputs resident in HBM).  At N > 1 (one process per GPU
-under torch.distributed.run) every rank renders its own frame of a camera path, so per-GPU
-work is fixed and there is no data-path collective ("scaling": "weak"); the barrier and the
-max-over-ranks timing are the only cross-rank operations in the timed region.
+One step = one frame of the configuration (C2 by default), inputs resident in HBM.
 
-Rank 0 prints ONE JSON line.  `roofline` is the algorithmic-byte rate of the trace kernel
-(SURVEY.md §8d units x counts from a counting pass, / the kernel's average duration measured
-with HIP events on its stream in the timed loop); `cpu_baseline` is the CPU oracle
-(oracle/, fast mode) timed on this host on the same workload.
+* N = 1: the frame loop of the C-ABI (trt_render_frames, 2 frames in flight) on one GPU.
+* N > 1 (one process per GPU under torch.distributed.run): every frame is row-tiled over the
+  N GPUs and gathered over RCCL by the native multi-GPU path (trt_render_multi_frames,
+  csrc/trt_multi.cpp): strong scaling, the frame is fixed and each GPU renders 1/N of it.
+  Frames are gathered in batches of --frames-per-gather on a rotating root (batch j on rank
+  j % N).  The frame-per-GPU weak-scaling number is reported beside it (`weak_scaling`).
+
+Rank 0 prints ONE JSON line.  Extra keys: `tiled_frame` (BASELINE configs[3]: a 3840x2160
+~100k-triangle frame row-tiled over the N GPUs and gathered on rank 0 over RCCL, with its
+SHA-256 checked against the 1-GPU frame and the committed hash), `shipped_frame` (the
+reference's own default frame, config.hpp:97-101 at MAX_DEPTH 20), `readme_frame` (the scene
+of the reference's only published frame rate, README.md:334-340), `roofline` (FP32 VALU:
+SURVEY §8d flop units x this frame's counted work / the kernel's HIP-event launch time),
+`cpu_baseline` (the CPU oracle timed on this host on the same workload).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
-import math
 import os
 import statistics
 import sys
@@ -28,9 +34,11 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector, FMA = 2 flops (AMD spec)
 TIME_EVERY = 16  # one timed (event-bracketed) launch per 16 frames
+FRAME_HASHES = REPO / "tests" / "golden" / "frame_hashes.json"
+METRIC = "Mray/s (primary+secondary) at 1024×768 depth4; 1/2/4/8-GPU scaling"
 
 
 def parse():
@@ -38,15 +46,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5", "ref"])
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5", "ref", "readme"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight (trt_set_frames_in_flight; the reference's MAX_FRAMES_IN_FLIGHT = 2)")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (trt_set_subtree_split: 0 auto, 1 off)")
-    ap.add_argument("--pmc", default=None, help="PMC summary json (tools/pmc_traffic.py) for roofline.traffic")
+    ap.add_argument("--band-rows", type=int, default=8, help="rows per band of the tiled frames")
+    ap.add_argument("--frames-per-gather", type=int, default=8,
+                    help="frames whose bands move in one RCCL gather (N > 1 headline)")
     ap.add_argument("--tiled-frames", type=int, default=20,
-                    help="frames of the tiled-frame leg (C4 row-tiled over the ranks + RCCL gather); 0 skips it")
+                    help="frames of the tiled 3840x2160 leg (C4 row-tiled + RCCL gather on rank 0); 0 skips it")
+    ap.add_argument("--extra-frames", type=int, default=40,
+                    help="frames of the shipped / README-scene legs; 0 skips them")
     return ap.parse_args()
 
 
@@ -57,19 +69,45 @@ WORKLOADS = {
     "C5": "3840x2160, C4 scene, 16 jittered spp, depth 4",
     "ref": "1024x768, the shipped frame: glass + water + ice (37,956 tris / 594 batches), floor, "
            "7616x3808 seeded envmap, depth 20 (config.hpp:97-101, shader.comp:75-84)",
+    "readme": "1024x768, the README-era scene: asschercut + bunny + dragon + venus + fudanlogo "
+              "(53,877 tris / 844 batches, config.hpp:96), checker floor, envmap, depth 20",
 }
 
 
+def make_scene(name: str):
+    from vkcomputeshader_tinyraytracer_amd import scene as S
+
+    if name == "ref":
+        return S.config_reference_default()
+    if name == "readme":
+        return S.config_readme()
+    return S.CONFIGS[name]()
+
+
+# ---- roofline units ---------------------------------------------------------
+
+def algorithmic_flops(st: dict, pixels: int, envmap: bool, mesh: bool) -> int:
+    """FP32 flops of the work the kernel executed, in SURVEY §8(d) units: slab test 24 per box
+    (BVH / hierarchy node or the reference's batch gate), Moller-Trumbore 22 / 34 / 52 / 59 by
+    the stage it exits at (+27 for the hit's interpolated normal), sphere test 21, floor test 8,
+    invDir 3 per mesh query, Phong 60 per light (3 lights per hit segment), background uv +
+    bilinear 40 per envmap miss.  Child-ray construction and gamma are not counted."""
+    queries = st["primary_rays"] + st["secondary_rays"] + st["shadow_rays"]
+    scene_queries = st["primary_rays"] + st["secondary_rays"]
+    hits = scene_queries - st["misses"]
+    mt = (22 * st["tri_tests"] + 12 * st["tri_past_a"] + 18 * st["tri_past_u"] + 7 * st["tri_past_v"])
+    return int(24 * (st["node_tests"] + st["batch_tests"]) + mt + 27 * st["tri_nearest"]
+               + 21 * st["sphere_tests"] + 8 * scene_queries + (3 * queries if mesh else 0)
+               + 180 * hits + (40 * st["misses"] if envmap else 0))
+
+
 def algorithmic_bytes(st: dict, pixels: int, envmap: bool) -> int:
-    """SURVEY.md §8(d) units: 24 B per batch (or hierarchy-node) bbox tested (+8 B start/count
-    when a batch passes),
-    36 B per triangle tested (v0, e1, e2), 16 B per sphere tested, 16 B per envmap sample
-    (4 RGBA8 texels), 48 B material per closest hit (+36 B vertex normals for a triangle),
-    4 B written per pixel."""
-    hits = st["primary_rays"] + st["secondary_rays"] - st["misses"]
-    return (24 * (st["batch_tests"] + st.get("node_tests", 0)) + 8 * st["batch_hits"] + 36 * st["tri_tests"]
-            + 16 * st["sphere_tests"] + (16 * st["misses"] if envmap else 0)
-            + 48 * hits + 36 * st["tri_nearest"] + 4 * pixels)
+    """SURVEY §8(d) byte units for the data that lives in memory (sphere records and the floor /
+    sphere materials are kernel arguments in SGPRs and are excluded): 24 B per box tested,
+    +8 B start/count per batch passed, 36 B per triangle tested, 16 B per envmap sample,
+    48 B material + 36 B vertex normals per triangle hit, 4 B written per pixel."""
+    return int(24 * (st["batch_tests"] + st["node_tests"]) + 8 * st["batch_hits"] + 36 * st["tri_tests"]
+               + (16 * st["misses"] if envmap else 0) + 84 * st["tri_nearest"] + 4 * pixels)
 
 
 def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
@@ -99,180 +137,247 @@ def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
     }
 
 
-def tiled_frame(frames: int, rank: int, world: int, dist, dev: int) -> dict:
-    """BASELINE configs[3]: a 3840x2160 C4 frame row-tiled across the ranks (interleaved
-    8-row bands, dist.TiledFrame) and gathered to rank 0 as RGBA8 over RCCL (xGMI), then
-    re-interleaved there.  Strong scaling: the frame is fixed, each rank renders 1/N of it.
-    Two frames in flight (dist.PipelinedTiles, main.cpp:45): frame i's gather and render
-    overlap frame i+1's render.  The timed region (barrier + synchronize on both sides, max over ranks)
-    covers `frames` frames end to end.  `frame_sha256` (rank 0's last assembled frame) is the
-    same at every world size: the tiled frame is bit-identical to the 1-GPU frame."""
-    import hashlib
+class Group:
+    """torch.distributed helpers (no-ops at N = 1)."""
 
+    def __init__(self, world: int, rank: int):
+        self.world, self.rank = world, rank
+        self.dist = None
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, "MAX")
+
+    def sum(self, x: float) -> float:
+        return self._reduce(x, "SUM")
+
+    def _reduce(self, x: float, op: str) -> float:
+        if not self.dist:
+            return x
+        import torch
+
+        t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
+        return float(t.item())
+
+    def unique_id(self) -> bytes:
+        from vkcomputeshader_tinyraytracer_amd.multi import unique_id
+
+        obj = [unique_id() if self.rank == 0 else None]
+        if self.dist:
+            self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed(g: Group, fn) -> float:
+    """Barrier + synchronize on both sides; the max over ranks of the wall time."""
+    import torch
+
+    torch.cuda.synchronize()
+    g.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    g.barrier()
+    return g.max(time.perf_counter() - t0)
+
+
+def frame_loop(dev: int, scene, frames: int, warmup: int, inflight: int, split: int, time_every: int = TIME_EVERY,
+               g: Group | None = None):
+    """trt_render_frames of `scene` on one GPU: (elapsed s, kernel ms per sampled launch, stats of
+    a counting pass, params)."""
     import torch
 
     import vkcomputeshader_tinyraytracer_amd as trt
-    from vkcomputeshader_tinyraytracer_amd import dist as D, scene as S
 
-    band = 8
-    sc = S.config_c4()
-    p = sc.params()
+    p = scene.params()
     r = trt.Renderer(dev)
-    r.upload_scene(sc)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    r.set_stream(streams[0])
-    pipe = D.PipelinedTiles(p.width, p.height, band, torch.device("cuda", dev), streams)
-    bp = D.band_params(p, band, world, rank)
-    _, _, st = r.draw_frame(bp, out8=pipe.tf[0].local, count=True)
-    torch.cuda.synchronize()
-    rays = st["primary_rays"] + st["secondary_rays"]
-
-    def render(out, stream):  # frames alternate between two streams: consecutive renders overlap
+    try:
+        r.upload_scene(scene)
+        r.set_subtree_split(split)
+        _, _, st = r.draw_frame(p, count=True)  # counting pass, excluded from timing
+        out8 = torch.empty((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.Stream()
         r.set_stream(stream)
-        r.draw_frame(bp, out8=out)
+        r.set_frames_in_flight(max(1, inflight))
+        r.render_frames(p, out8, warmup)
+        box = {}
+        elapsed = timed(g or Group(1, 0), lambda: box.update(n=r.render_frames(p, out8, frames, timing=True,
+                                                                                 time_every=time_every)))
+        kern_ms = r.frame_times(box["n"])
+        return elapsed, kern_ms, st, p
+    finally:
+        r.close()
 
-    for _ in range(4):
-        pipe.submit(render)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(frames):
-        img = pipe.submit(render)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed, rays = float(mx[0].item()), int(t[1].item())
-    out = None
-    if rank == 0:
-        sha = hashlib.sha256(img.contiguous().cpu().numpy().tobytes()).hexdigest()
-        out = {
+
+def extra_frame(dev: int, name: str, frames: int, args) -> dict:
+    import vkcomputeshader_tinyraytracer_amd  # noqa: F401  (lib load)
+
+    sc = make_scene(name)
+    elapsed, kern_ms, st, p = frame_loop(dev, sc, frames, 4, args.inflight, args.split, time_every=4)
+    rays = st["primary_rays"] + st["secondary_rays"]
+    ms = elapsed / frames * 1e3
+    out = {
+        "workload": f"{name}: {WORKLOADS[name]}",
+        "frames": frames,
+        "frames_in_flight": args.inflight,
+        "ms_per_frame": round(ms, 4),
+        "fps": round(1e3 / ms, 2),
+        "mray_s": round(rays / (ms * 1e-3) / 1e6, 3),
+        "rays_per_frame": rays,
+        "shadow_rays_per_frame": st["shadow_rays"],
+        "kernel_span_ms": round(float(kern_ms.mean()), 4),
+    }
+    if name == "readme":
+        out["published_context"] = {
+            "fps": "10-11 (dips to 7)", "hardware": "NVIDIA GeForce RTX 4060", "source": "README.md:334-340",
+            "note": "same scene and size, but an older shader state of the reference: a different-hardware "
+                    "context bar, not a like-for-like baseline",
+            "ratio_vs_10.5_fps": round(1e3 / ms / 10.5, 1),
+        }
+    return out
+
+
+def tiled_stream(g: Group, dev: int, multi, scene, frames: int, warmup: int, band_rows: int, root: int,
+                 per_gather: int):
+    """trt_render_multi_frames of `scene` over all ranks: (elapsed s, whole-frame stats, output)."""
+    import torch
+
+    p = scene.params()
+    multi.upload_scene(scene if g.rank == 0 else None)
+    st = multi.draw_frame(p, band_rows=band_rows, root=0, count=True)  # counting pass (all ranks)
+    out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    multi.set_stream(0, stream)
+    multi.render_frames(p, warmup, band_rows, root, per_gather, outs=[out])
+    elapsed = timed(g, lambda: multi.render_frames(p, frames, band_rows, root, per_gather, outs=[out]))
+    multi.set_stream(0, None)
+    return elapsed, st, out, p
+
+
+def tiled_frame(g: Group, dev: int, multi, frames: int, band_rows: int) -> dict:
+    """BASELINE configs[3]: a 3840x2160 C4 frame row-tiled across the ranks (interleaved
+    band_rows-row bands) and gathered to rank 0 as RGBA8 over RCCL (xGMI) by the native path,
+    one gather per frame (the display case), two frames in flight."""
+    import torch
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+    from vkcomputeshader_tinyraytracer_amd import scene as S
+
+    sc = S.config_c4()
+    elapsed, st, out, p = tiled_stream(g, dev, multi, sc, frames, 2, band_rows, 0, 1)
+    rays = st["primary_rays"] + st["secondary_rays"]
+    res = None
+    if g.rank == 0:
+        sha = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
+        with trt.Renderer(dev) as r:  # the 1-GPU frame (trt_render of the whole frame)
+            r.upload_scene(sc)
+            one, _, _ = r.draw_frame(p)
+        sha1 = hashlib.sha256(one.tobytes()).hexdigest()
+        committed = json.loads(FRAME_HASHES.read_text()).get("C4_3840x2160") if FRAME_HASHES.exists() else None
+        res = {
             "workload": "C4: 3840x2160, 20 icospheres (102,400 tris), depth 4, one frame row-tiled "
-                        f"over {world} GPU(s) in interleaved {band}-row bands",
+                        f"over {g.world} GPU(s) in interleaved {band_rows}-row bands, gathered on rank 0",
             "scaling": "strong",
-            "collective": "dist.gather of padded RGBA8 band buffers to rank 0 (RCCL over xGMI), "
-                          "overlapped with the next frame's render (2 frames in flight on 2 render streams)"
-                          if world > 1 else "none (1 GPU)",
+            "collective": "RCCL grouped ncclSend/ncclRecv of the compact RGBA8 band buffers to rank 0 "
+                          "(csrc/trt_multi.cpp)" + (" — 1 rank: sent to itself" if g.world == 1 else ""),
             "frames": frames,
             "ms_per_frame": round(elapsed / frames * 1e3, 4),
             "frames_per_s": round(frames / elapsed, 3),
             "mray_s": round(rays * frames / elapsed / 1e6, 3),
             "rays_per_frame": rays,
-            "gather_bytes_per_frame": int(pipe.tf[0].local.numel() * world) if world > 1 else 0,
+            "gather_bytes_per_frame": int(p.width * p.height * 4 * (g.world - 1) / g.world),
             "frame_sha256": sha,
+            "matches_1gpu_frame": sha == sha1,
+            "matches_committed_hash": (sha == committed) if committed else None,
         }
-    r.close()
-    return out
+    torch.cuda.synchronize()
+    return res
 
 
 def main():
     args = parse()
-    import numpy as np
     import torch
-
-    import vkcomputeshader_tinyraytracer_amd as trt
-    from vkcomputeshader_tinyraytracer_amd import scene as S, types as T
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(local if world > 1 else 0)
     dev = torch.cuda.current_device()
+    g = Group(world, rank)
 
-    scene = S.config_reference_default() if args.config == "ref" else S.CONFIGS[args.config]()
-    # Weak scaling: rank r renders frame r of a short camera path (camPos drifts along x).
-    scene.ubo = S.make_ubo(cam=(0.05 * rank, 0.0, 0.0))
-    params = scene.params()
-    rows = params.height
-    pixels = rows * params.width
-    envmap = bool(params.flags & T.FLAG_ENVMAP)
+    import vkcomputeshader_tinyraytracer_amd as trt
+    from vkcomputeshader_tinyraytracer_amd import types as T
+    from vkcomputeshader_tinyraytracer_amd.multi import ROOT_ROTATE, MultiRenderer
 
-    r = trt.Renderer(dev)
-    r.upload_scene(scene)
-    out8 = torch.empty((rows, params.width, 4), dtype=torch.uint8, device="cuda")
-
-    # Counting pass (excluded from timing): rays and per-stage work of this rank's frame.
-    _, _, st = r.draw_frame(params, count=True)
-    rays_per_frame = st["primary_rays"] + st["secondary_rays"]
-    alg_bytes = algorithmic_bytes(st, pixels, envmap)
-
-    # Frames are enqueued by the native frame loop (trt_render_frames: one kernel launch per
-    # frame).  A HIP event pair on the kernel's own stream brackets every TIME_EVERY-th launch:
-    # the kernel duration is measured live while the timed region stays nearly event-free
-    # (an event pair adds ~7 us of queue time to a ~40 us frame).
-    # Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT = 2): frame i runs on slot
-    # i % inflight, so frame i+1's tiles fill the GPU while frame i's slowest tiles finish;
-    # render_frames joins every slot back into `stream` before it returns.  Every step renders
-    # the same frame, so the frames share one image (the reference's single storage image,
-    # main.cpp:865-926; concurrent frames write identical bytes).
-    nfl = max(1, args.inflight)
-    stream = torch.cuda.Stream()
-    r.set_stream(stream)
-    r.set_frames_in_flight(nfl)
-    r.set_subtree_split(args.split)
-    r.render_frames(params, out8, args.warmup)
-    torch.cuda.synchronize()
-
+    scene = make_scene(args.config)
     K = args.steps
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ntimed = r.render_frames(params, out8, K, timing=True, time_every=TIME_EVERY)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kern_ms = r.frame_times(ntimed)
-    kern_avg_ms = float(kern_ms.mean())
+    envmap = bool(scene.flags & T.FLAG_ENVMAP)
+    mesh = len(scene.models) > 0
 
-    total_rays = rays_per_frame
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        rr = torch.tensor([rays_per_frame], dtype=torch.float64, device="cuda")
-        dist.all_reduce(rr, op=dist.ReduceOp.SUM)
-        total_rays = int(rr.item())
-        kk = torch.tensor([kern_avg_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(kk, op=dist.ReduceOp.MAX)
-        kern_avg_ms = float(kk.item())
+    # Frame per GPU (the N = 1 headline; the weak-scaling extra at N > 1): also the live kernel
+    # timing of the roofline.
+    elapsed1, kern_ms, st, params = frame_loop(dev, scene, K, args.warmup, args.inflight, args.split, g=g)
+    rays_per_frame = st["primary_rays"] + st["secondary_rays"]
+    pixels = params.width * params.height
+    kern_avg_ms = g.max(float(kern_ms.mean()))
+    weak_value = g.sum(rays_per_frame) * K / elapsed1 / 1e6
 
-    value = total_rays * K / elapsed / 1e6
-    ms_per_step = elapsed / K * 1e3
-    tiled = None
-    if args.tiled_frames > 0:
-        try:
-            tiled = tiled_frame(args.tiled_frames, rank, world, dist, dev)
-        except Exception as e:  # the headline line is still printed; the failure is reported in it
-            tiled = {"error": f"{type(e).__name__}: {e}"} if rank == 0 else None
+    multi = MultiRenderer.for_rank(dev, world, rank, g.unique_id())
+    if world == 1:
+        value, ms_per_step = weak_value, elapsed1 / K * 1e3
+        scaling, parallelism = "weak", "1 GPU"
+        headline_extra = None
+    else:
+        # the frame row-tiled over all GPUs, RCCL gathers of --frames-per-gather frames on a rotating root
+        elapsed, mst, _, _ = tiled_stream(g, dev, multi, scene, K, args.warmup, args.band_rows, ROOT_ROTATE,
+                                          args.frames_per_gather)
+        rays_whole = mst["primary_rays"] + mst["secondary_rays"]
+        value, ms_per_step = rays_whole * K / elapsed / 1e6, elapsed / K * 1e3
+        scaling = "strong"
+        parallelism = (f"row-tiled x{world} ({args.band_rows}-row interleaved bands), RCCL gather of "
+                       f"{args.frames_per_gather} frames per op on a rotating root")
+        headline_extra = {"weak_scaling": {
+            "value": round(weak_value, 3), "unit": "Mray/s",
+            "workload": f"frame per GPU: every rank renders its own whole {args.config} frame, no data-path collective",
+            "ms_per_step": round(elapsed1 / K * 1e3, 5)}}
+
+    tiled = tiled_frame(g, dev, multi, args.tiled_frames, args.band_rows) if args.tiled_frames > 0 else None
+    multi.close()
+
+    extras = {}
+    if args.extra_frames > 0:
+        for key, name in (("shipped_frame", "ref"), ("readme_frame", "readme")):
+            if rank == 0:
+                if world == 1:
+                    try:
+                        extras[key] = extra_frame(dev, name, args.extra_frames, args)
+                    except Exception as e:  # N = 1: report the failure in the line
+                        extras[key] = {"error": f"{type(e).__name__}: {e}"}
+                else:  # N > 1: fail fast (the launcher tears the job down)
+                    extras[key] = extra_frame(dev, name, args.extra_frames, args)
+            g.barrier()
 
     if rank == 0:
-        achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_path = Path(args.pmc) if args.pmc else REPO / "profiles" / f"pmc_{args.config}.json"
-        if pmc_path.exists():
-            try:
-                traffic = json.loads(pmc_path.read_text()).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        flops = algorithmic_flops(st, pixels, envmap, mesh)
+        tflops = flops / (kern_avg_ms * 1e-3) / 1e12
+        abytes = algorithmic_bytes(st, pixels, envmap)
         result = {
-            "metric": "Mray/s (primary+secondary) at 1024\u00d7768 depth4; 1/2/4/8-GPU scaling",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mray/s",
             "n_gpus": world,
@@ -280,7 +385,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded procedural envmap; reference spheres/lights/materials, main.cpp:125-143)",
@@ -292,36 +397,43 @@ def main():
                 "spp": params.spp,
                 "rays_per_frame": rays_per_frame,
                 "shadow_rays_per_frame": st["shadow_rays"],
-                "parallelism": f"frame-per-GPU x{world}" if world > 1 else "1 GPU",
-                "frames_in_flight": nfl,
+                "parallelism": parallelism,
+                "frames_in_flight": args.inflight,
             },
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "bound": "valu",
+                "achieved": round(tflops, 3),
+                "peak": VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(tflops / VALU_PEAK_TFLOPS, 4),
+                "traffic": None,
                 "kernel": "trace_kernel",
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "per_frame_rate": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
-                "note": "achieved = algorithmic SoA bytes (SURVEY §8d) per launch / HIP-event kernel "
-                        "time on the launch's stream (with frames in flight the span includes the "
-                        "overlapping frame); per_frame_rate = the same bytes / wall time per frame. "
-                        "An efficiency index, not physical traffic (wave-uniform scalar/L2 reuse); "
-                        "physical HBM bytes per launch = traffic (PMC FETCH_SIZE + WRITE_SIZE)",
+                "flops_per_launch": flops,
+                "note": "FP32 flops of the executed work in SURVEY §8d units (counting pass of this frame) / "
+                        "the trace kernel's launch time (HIP events on its stream, every 16th launch of the "
+                        "timed loop; with 2 frames in flight a launch's span includes the overlapping frame); "
+                        "peak counts an FMA as 2 flops, the kernel has no FMA contraction (-ffp-contract=off). "
+                        "traffic: no PMC pass in this run (profiles/ holds the PMC summaries of this build)",
+                "hbm_index": {
+                    "algorithmic_bytes_per_launch": abytes,
+                    "gb_s_per_launch": round(abytes / (kern_avg_ms * 1e-3) / 1e9, 2),
+                    "gb_s_per_frame": round(abytes / (elapsed1 / K) / 1e9, 2),
+                    "peak": HBM_PEAK_GBS,
+                    "note": "SURVEY §8d bytes excluding SGPR-resident sphere records and constant materials; "
+                            "an index, not measured traffic",
+                },
             },
         }
+        if headline_extra:
+            result.update(headline_extra)
         if tiled is not None:
             result["tiled_frame"] = tiled
+        result.update(extras)
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(scene, params, rays_per_frame, args.cpu_seconds)
         print(json.dumps(result), flush=True)
-
-    r.close()
-    if dist:
-        dist.destroy_process_group()
+    g.close()
 
 
 if __name__ == "__main__":

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define TRT_ABI_VERSION 1
+#define TRT_ABI_VERSION 2
 
 /* status codes */
 #define TRT_OK 0
@@ -96,6 +96,11 @@ typedef struct trt_stats {
                                 reference's linear loop; batch_tests then counts only the batch
                                 boxes actually reached) */
     double kernel_ms;        /* device time of the frame (TRT_FLAG_TIMING) */
+    /* Moller-Trumbore stages reached (shader.comp:223-270; the per-stage FP32 work of the VALU
+     * roofline, SURVEY §8d: 22 / 34 / 52 / 59 flops at exit after a / u / v / t): */
+    uint64_t tri_past_a;     /* triangle tests past the parallel test (u computed) */
+    uint64_t tri_past_u;     /* ... past the u test (v computed) */
+    uint64_t tri_past_v;     /* ... past the v test (t computed) */
 } trt_stats;
 
 typedef struct trt_ctx trt_ctx;

@@ -142,6 +142,9 @@ enum : int { HIT_NONE = 0, HIT_FLOOR = 1, HIT_SPHERE = 2, HIT_TRI = 3 };
 // Per-lane work counters (COUNT builds only): the units of trt_stats.
 struct Cnt {
     uint32_t pri = 0, sec = 0, sh = 0, miss = 0, trin = 0, sph = 0, bt = 0, bh = 0, tt = 0, nt = 0;
+    // Moller-Trumbore stages reached (the FP32 work units of the VALU roofline):
+    // past the parallel test, past the u test, past the v test (t computed)
+    uint32_t ta = 0, tu = 0, tv = 0;
 #ifdef TRT_DIAG_PIXEL_WORK
     uint32_t wn = 0, wt = 0, wseg = 0, wmax = 0; // diagnostic: this lane's node visits, tri tests, segments, max nodes/query
 #endif
@@ -246,13 +249,16 @@ __device__ __forceinline__ void walk_batches(const KArgs& A, f3 o, f3 d, f3 inv,
                         f3 hv = cross3(d, e2);
                         float a = dot3(e1, hv);
                         if (a > -TRT_EPS && a < TRT_EPS) continue;
+                        if (COUNT) ++c.ta;
                         float f = rcp_rn_lane(a);
                         f3 sv = sub(o, v0);
                         float u = f * dot3(sv, hv);
                         if (u < 0.0f || u > 1.0f) continue;
+                        if (COUNT) ++c.tu;
                         f3 q = cross3(sv, e1);
                         float v = f * dot3(d, q);
                         if (v < 0.0f || u + v > 1.0f) continue;
+                        if (COUNT) ++c.tv;
                         float t = f * dot3(e2, q);
                         if (t <= TRT_EPS) continue;
                         if (SHADOW) {
@@ -419,13 +425,16 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
                 f3 hv = cross3(d, e2);
                 float a = dot3(e1, hv);
                 if (a > -TRT_EPS && a < TRT_EPS) continue;
+                        if (COUNT) ++c.ta;
                 float f = rcp_rn_lane(a);
                 f3 sv = sub(o, v0);
                 float u = f * dot3(sv, hv);
                 if (u < 0.0f || u > 1.0f) continue;
+                        if (COUNT) ++c.tu;
                 f3 q = cross3(sv, e1);
                 float v = f * dot3(d, q);
                 if (v < 0.0f || u + v > 1.0f) continue;
+                        if (COUNT) ++c.tv;
                 float t = f * dot3(e2, q);
                 if (t <= TRT_EPS) continue;
                 const uint32_t tri = __float_as_uint(g.pad[0]), batch = __float_as_uint(g.pad[1]);
@@ -482,13 +491,16 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
         f3 hv = cross3(d, e2);
         float a = dot3(e1, hv);
         if (a > -TRT_EPS && a < TRT_EPS) continue;
+                        if (COUNT) ++c.ta;
         float f = rcp_rn_lane(a);
         f3 sv = sub(o, v0);
         float u = f * dot3(sv, hv);
         if (u < 0.0f || u > 1.0f) continue;
+                        if (COUNT) ++c.tu;
         f3 q = cross3(sv, e1);
         float v = f * dot3(d, q);
         if (v < 0.0f || u + v > 1.0f) continue;
+                        if (COUNT) ++c.tv;
         float t = f * dot3(e2, q);
         if (t <= TRT_EPS) continue;
         const uint32_t tri = __float_as_uint(cur.pad[0]), batch = __float_as_uint(cur.pad[1]);
@@ -1280,9 +1292,10 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
 #endif
 
 __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
-    const uint32_t v[10] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt};
+    const uint32_t v[13] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt,
+                            cnt.ta, cnt.tu, cnt.tv};
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < 13; ++i) {
         unsigned long long w = wave_sum((unsigned long long)v[i]);
         if (lane_id() == 0) atomicAdd(&A.counters[i], w);
     }

@@ -135,7 +135,7 @@ bool row_selected(const trt_params* p, uint32_t r) {
 
 extern "C" {
 
-const char* trt_version(void) { return "trt-mi355x 0.1 (gfx950, abi 1)"; }
+const char* trt_version(void) { return "trt-mi355x 0.2 (gfx950, abi 2)"; }
 
 void trt_params_default(trt_params* p) {
     if (!p) return;
@@ -736,6 +736,9 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
         st->batch_hits = cnt[7];
         st->tri_tests = cnt[8];
         st->node_tests = cnt[9];
+        st->tri_past_a = cnt[10];
+        st->tri_past_u = cnt[11];
+        st->tri_past_v = cnt[12];
         st->kernel_ms = 0.0;
         if (timing) {
             float ms = 0.0f;

@@ -361,4 +361,17 @@ def config_reference_default(meshes: dict | None = None, env_size=(7616, 3808), 
                  flags=T.FLAGS_REFERENCE)
 
 
+def config_readme(meshes: dict | None = None, env_size=(7616, 3808), width=1024, height=768,
+                  max_depth=20) -> Scene:
+    """The README-era scene that carries the reference's only published frame rate (10-11 FPS
+    on an RTX 4060 at 1024x768, README.md:334-340): asschercut + bunny + dragon + venus +
+    fudanlogo (config.hpp:96; 53,877 tris / 844 batches, rotated and flat-shaded models),
+    checker floor, spheres off, envmap background, MAX_DEPTH 20 (shader.comp:75).  The README
+    screenshots come from an older shader state, so the published figure is context only."""
+    meshes = meshes if meshes is not None else load_golden_meshes()
+    tris, models = build_models(README_MODEL_LIST, meshes)
+    return Scene("readme", make_ubo(), tris, models, cached_envmap(*env_size), width, height, max_depth,
+                 flags=T.FLAG_FLOOR | T.FLAG_CHECKER | T.FLAG_ENVMAP | T.FLAG_ROW_QUIRK)
+
+
 CONFIGS = {"C1": config_c1, "C2": config_c2, "C3": config_c3, "C4": config_c4, "C5": config_c5}

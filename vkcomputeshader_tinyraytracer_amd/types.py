@@ -105,10 +105,14 @@ class Stats(ctypes.Structure):
         ("tri_tests", ctypes.c_uint64),
         ("node_tests", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double),
+        ("tri_past_a", ctypes.c_uint64),
+        ("tri_past_u", ctypes.c_uint64),
+        ("tri_past_v", ctypes.c_uint64),
     ]
 
     COUNTERS = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
-                "sphere_tests", "batch_tests", "batch_hits", "tri_tests", "node_tests")
+                "sphere_tests", "batch_tests", "batch_hits", "tri_tests", "node_tests",
+                "tri_past_a", "tri_past_u", "tri_past_v")
     # counters that must equal the oracle's (the reference's work); batch_tests / node_tests
     # depend on the traversal (the kernel culls with a conservative hierarchy)
     EXACT = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
@@ -122,7 +126,7 @@ class Stats(ctypes.Structure):
         return d
 
 
-assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 88
+assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 112
 
 
 def make_params(
