@@ -87,18 +87,25 @@ def make_scene(name: str):
 # ---- roofline units ---------------------------------------------------------
 
 def algorithmic_flops(st: dict, pixels: int, envmap: bool, mesh: bool) -> int:
-    """FP32 flops of the work the kernel executed, in SURVEY §8(d) units: slab test 24 per box
+    """FP32 flops of the work the frame executes, in SURVEY §8(d) units: slab test 24 per box
     (BVH / hierarchy node or the reference's batch gate), Moller-Trumbore 22 / 34 / 52 / 59 by
     the stage it exits at (+27 for the hit's interpolated normal), sphere test 21, floor test 8,
     invDir 3 per mesh query, Phong 60 per light (3 lights per hit segment), background uv +
-    bilinear 40 per envmap miss.  Child-ray construction and gamma are not counted."""
+    bilinear 40 per envmap miss.  Child-ray construction and gamma are not counted; the work
+    of the shadow queries the frame skips (zero contribution, counted by the counting pass) is
+    subtracted."""
     queries = st["primary_rays"] + st["secondary_rays"] + st["shadow_rays"]
     scene_queries = st["primary_rays"] + st["secondary_rays"]
     hits = scene_queries - st["misses"]
     mt = (22 * st["tri_tests"] + 12 * st["tri_past_a"] + 18 * st["tri_past_u"] + 7 * st["tri_past_v"])
-    return int(24 * (st["node_tests"] + st["batch_tests"]) + mt + 27 * st["tri_nearest"]
-               + 21 * st["sphere_tests"] + 8 * scene_queries + (3 * queries if mesh else 0)
-               + 180 * hits + (40 * st["misses"] if envmap else 0))
+    total = (24 * (st["node_tests"] + st["batch_tests"]) + mt + 27 * st["tri_nearest"]
+             + 21 * st["sphere_tests"] + 8 * scene_queries + (3 * queries if mesh else 0)
+             + 180 * hits + (40 * st["misses"] if envmap else 0))
+    # the counting pass traces the shadow queries the frame skips (zero contribution): not executed
+    skipped = (24 * st["skipped_box_tests"] + 22 * st["skipped_tri_tests"] + 12 * st["skipped_tri_past_a"]
+               + 18 * st["skipped_tri_past_u"] + 7 * st["skipped_tri_past_v"] + 21 * st["skipped_sphere_tests"]
+               + (3 * st["shadow_skipped"] if mesh else 0))
+    return int(total - skipped)
 
 
 def algorithmic_bytes(st: dict, pixels: int, envmap: bool) -> int:
@@ -106,7 +113,8 @@ def algorithmic_bytes(st: dict, pixels: int, envmap: bool) -> int:
     sphere materials are kernel arguments in SGPRs and are excluded): 24 B per box tested,
     +8 B start/count per batch passed, 36 B per triangle tested, 16 B per envmap sample,
     48 B material + 36 B vertex normals per triangle hit, 4 B written per pixel."""
-    return int(24 * (st["batch_tests"] + st["node_tests"]) + 8 * st["batch_hits"] + 36 * st["tri_tests"]
+    return int(24 * (st["batch_tests"] + st["node_tests"] - st["skipped_box_tests"]) + 8 * st["batch_hits"]
+               + 36 * (st["tri_tests"] - st["skipped_tri_tests"])
                + (16 * st["misses"] if envmap else 0) + 84 * st["tri_nearest"] + 4 * pixels)
 
 
@@ -240,6 +248,7 @@ def extra_frame(dev: int, name: str, frames: int, args) -> dict:
         "mray_s": round(rays / (ms * 1e-3) / 1e6, 3),
         "rays_per_frame": rays,
         "shadow_rays_per_frame": st["shadow_rays"],
+        "shadow_rays_traced_per_frame": st["shadow_rays"] - st["shadow_skipped"],
         "kernel_span_ms": round(float(kern_ms.mean()), 4),
     }
     if name == "readme":
@@ -397,6 +406,7 @@ def main():
                 "spp": params.spp,
                 "rays_per_frame": rays_per_frame,
                 "shadow_rays_per_frame": st["shadow_rays"],
+                "shadow_rays_traced_per_frame": st["shadow_rays"] - st["shadow_skipped"],
                 "parallelism": parallelism,
                 "frames_in_flight": args.inflight,
             },

@@ -101,6 +101,13 @@ typedef struct trt_stats {
     uint64_t tri_past_a;     /* triangle tests past the parallel test (u computed) */
     uint64_t tri_past_u;     /* ... past the u test (v computed) */
     uint64_t tri_past_v;     /* ... past the v test (t computed) */
+    /* Shadow queries a frame does not trace: the light's diffuse and specular terms both vanish
+     * from the colour (zero term or zero albedo weight), so lit or shadowed it adds exactly
+     * nothing (shader.comp:495-505).  The counting pass traces them (every counter above is the
+     * reference's work) and reports them and the work inside them here: */
+    uint64_t shadow_skipped;
+    uint64_t skipped_sphere_tests, skipped_box_tests, skipped_tri_tests;
+    uint64_t skipped_tri_past_a, skipped_tri_past_u, skipped_tri_past_v;
 } trt_stats;
 
 typedef struct trt_ctx trt_ctx;

@@ -320,7 +320,8 @@ def test_overlapping_batches_fall_back_to_walk(gpu_renderer):
 def test_bvh_four_wave_build_bit_identical(gpu_renderer, golden_meshes, monkeypatch):
     """The BVH walk compiled for 4 waves per SIMD (GEOM 3, picked for large meshes; forced here
     with TRT_BVH_WAVES4, read at trt_create) renders exactly what the 3-wave build renders:
-    images, rayOut and every counter, with and without the subtree split."""
+    images, rayOut and the reference-work counters, with and without the subtree split.  (The
+    4-wave build walks the quantized 64-B nodes, so its traversal work counters differ.)"""
     from vkcomputeshader_tinyraytracer_amd import Renderer
 
     scenes = [S.config_c3(240, 136, env_size=SMALL_ENV),
@@ -340,7 +341,7 @@ def test_bvh_four_wave_build_bit_identical(gpu_renderer, golden_meshes, monkeypa
         a8, a32, ast = out[key]
         b8, b32, bst = out[("1",) + key[1:]]
         assert np.array_equal(a8, b8) and np.array_equal(a32, b32), key
-        assert {k: v for k, v in ast.items() if k != "kernel_ms"} == {k: v for k, v in bst.items() if k != "kernel_ms"}
+        assert {k: ast[k] for k in T.Stats.EXACT} == {k: bst[k] for k in T.Stats.EXACT}
 
 
 def _cube():
@@ -417,3 +418,26 @@ def test_single_leaf_bvh_tests_each_triangle_once(gpu_renderer):
     assert wst["tri_tests"] > 0
     assert bst["tri_tests"] <= wst["tri_tests"] * 1.05 + 8, (bst, wst)
     _check(gpu_renderer, sc)
+
+
+@pytest.mark.parametrize("which", ["C2", "C3", "reference", "readme"])
+def test_skipped_dark_shadow_queries_exact(gpu_renderer, golden_meshes, which):
+    """A frame does not trace shadow queries whose light adds nothing lit or shadowed (zero
+    diffuse and specular terms, or zero albedo weights); the counting pass traces them and adds
+    their terms like the reference.  The two images are bit-identical, and the skipped
+    queries are reported."""
+    if which == "reference":
+        sc = S.config_reference_default(golden_meshes, env_size=SMALL_ENV, width=200, height=150)
+    elif which == "readme":
+        sc = S.config_readme(golden_meshes, env_size=SMALL_ENV, width=200, height=150)
+    else:
+        sc = S.CONFIGS[which](200, 150, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    for split in (1, 0):
+        gpu_renderer.set_subtree_split(split)
+        c8, c32, st = gpu_renderer.draw_frame(sc.params(), want32=True, count=True)
+        f8, f32, _ = gpu_renderer.draw_frame(sc.params(), want32=True)
+        assert np.array_equal(c8, f8) and np.array_equal(c32, f32), split
+    gpu_renderer.set_subtree_split(0)
+    assert 0 < st["shadow_skipped"] < st["shadow_rays"]
+    assert st["skipped_sphere_tests"] <= st["sphere_tests"] and st["skipped_tri_tests"] <= st["tri_tests"]

@@ -38,6 +38,8 @@ def main():
         kw = dict(width=a.width, height=a.height)
     if a.config == "ref":  # the shipped glass+water+ice frame
         sc = S.config_reference_default(**kw)
+    elif a.config == "readme":  # the README-era scene (config.hpp:96)
+        sc = S.config_readme(**kw)
     else:
         sc = S.CONFIGS[a.config](**kw)
     if a.depth:

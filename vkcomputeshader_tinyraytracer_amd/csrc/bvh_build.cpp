@@ -356,4 +356,59 @@ uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4
     return need.empty() ? 0 : need[0];
 }
 
+// Quantizes every BVH4 node's child boxes to 8-bit planes on a per-node grid (trt_device.h
+// Bvh4QNode).  Per axis the step is the power of two s >= extent / 250 of the node box [L, H]
+// and the origin p <= L - s (rounded down), so lower planes round down and upper planes round
+// up with one extra step of margin each.  Every quantized box is checked (exactly, in double)
+// to contain its padded child box; returns false (no quantized BVH) if one does not.
+bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out) {
+    out.assign(b4.size(), Bvh4QNode{});
+    for (size_t n = 0; n < b4.size(); ++n) {
+        const Bvh4Node& nd = b4[n];
+        Bvh4QNode& q = out[n];
+        const float* lo[3] = {nd.lox, nd.loy, nd.loz};
+        const float* hi[3] = {nd.hix, nd.hiy, nd.hiz};
+        q.exps = 0;
+        for (int a = 0; a < 3; ++a) {
+            double L = std::numeric_limits<double>::infinity(), H = -L;
+            for (int i = 0; i < 4; ++i) {
+                if (nd.child[i] == kBvh4None) continue;
+                if (!std::isfinite(lo[a][i]) || !std::isfinite(hi[a][i])) return false;
+                L = std::min(L, (double)lo[a][i]);
+                H = std::max(H, (double)hi[a][i]);
+            }
+            if (!(L <= H)) return false; // no used slot
+            const double ext = std::max(H - L, 1e-30);
+            int e = (int)std::ceil(std::log2(ext / 250.0));
+            while (std::ldexp(250.0, e) < ext) ++e; // guard log2 rounding
+            if (e < -126 || e > 127) return false;
+            const double sd = std::ldexp(1.0, e);
+            const double pd = L - sd;
+            float pf = (float)pd;
+            if ((double)pf > pd) pf = std::nextafter(pf, -std::numeric_limits<float>::infinity());
+            q.p[a] = pf;
+            q.exps |= (uint32_t)(e + 127) << (8 * a);
+            uint32_t wl = 0, wh = 0;
+            for (int i = 0; i < 4; ++i) {
+                uint32_t ql = 255, qh = 0; // unused slot: inverted box
+                if (nd.child[i] != kBvh4None) {
+                    const double fl = std::floor(((double)lo[a][i] - (double)pf) / sd) - 1.0;
+                    const double ch = std::ceil(((double)hi[a][i] - (double)pf) / sd) + 1.0;
+                    ql = (uint32_t)std::min(255.0, std::max(0.0, fl));
+                    qh = (uint32_t)std::min(255.0, std::max(0.0, ch));
+                    // exact containment check of the decoded planes
+                    if ((double)pf + ql * sd > (double)lo[a][i] || (double)pf + qh * sd < (double)hi[a][i]) return false;
+                }
+                wl |= ql << (8 * i);
+                wh |= qh << (8 * i);
+            }
+            q.qlo[a] = wl;
+            q.qhi[a] = wh;
+        }
+        q.pad[0] = q.pad[1] = 0;
+        for (int i = 0; i < 4; ++i) q.child[i] = nd.child[i];
+    }
+    return true;
+}
+
 } // namespace trt

@@ -24,6 +24,7 @@ struct trt_ctx {
     float4* d_nodes = nullptr; // implicit 8-ary hierarchy over the batches
     trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
     trt::Bvh4Node* d_bvh4 = nullptr; // the same, 4-wide
+    trt::Bvh4QNode* d_bvh4q = nullptr; // the same, 4-wide with quantized child boxes
     trt::TriGeo* d_bvh_tris = nullptr;
     uint32_t node_off[11] = {0};
     uint32_t top = 0;
@@ -70,7 +71,8 @@ struct trt_ctx {
     hipEvent_t fork_ev = nullptr;
     uint32_t fev_frames = 0;
     // bytes of each scene binding on the device (trt::kSceneBuf* order), for the broadcast
-    size_t scene_bytes[9] = {0};
+    size_t scene_bytes[10] = {0};
+    void* diag = nullptr; // diagnostic builds: ray-dump buffer (trt_diag_set_buffer)
 };
 
 namespace trt {
@@ -78,7 +80,7 @@ namespace trt {
 // The scene bindings of a context in a fixed order (the RCCL scene broadcast walks them).
 enum SceneBuf : int {
     kSceneBatches = 0, kSceneNodes, kSceneBvh, kSceneBvh4, kSceneBvhTris, kSceneGeo, kSceneShade,
-    kSceneMats, kSceneEnv, kSceneBufs
+    kSceneMats, kSceneEnv, kSceneBvh4Q, kSceneBufs
 };
 void** scene_buf(trt_ctx* c, int k);
 

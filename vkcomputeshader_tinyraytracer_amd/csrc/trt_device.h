@@ -75,6 +75,23 @@ struct alignas(16) Bvh4Node {
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node is 128 B");
 
+// The same 4-wide node with its child boxes quantized to 8 bits per plane (Ylitie et al.,
+// "Efficient incoherent ray traversal on GPUs through compressed wide BVHs", HPG 2017): a grid
+// of origin p and power-of-two step s = 2^(e - 127) per axis; child i's box is
+// [p + qlo_i * s, p + qhi_i * s], rounded outward by at least one step beyond the padded box
+// (bvh_build.cpp quantize_bvh4), so it stays conservative.  64 B = 4 x dwordx4 per visit
+// instead of 8.  Byte i of qlo[a] / qhi[a] belongs to child i; an unused slot has qlo = 255,
+// qhi = 0 on every axis (an inverted box, which the sign-ordered slab test never enters).
+struct alignas(16) Bvh4QNode {
+    float p[3];
+    uint32_t exps;   // e_x | e_y << 8 | e_z << 16 (biased exponents of the steps)
+    uint32_t qlo[3]; // per axis, 4 x u8 lower planes
+    uint32_t qhi[3]; // per axis, 4 x u8 upper planes
+    uint32_t pad[2];
+    uint32_t child[4];
+};
+static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode is 64 B");
+
 struct Mat {
     float albedo[4];
     float kd[3];
@@ -134,6 +151,7 @@ struct KArgs {
     unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
     const BvhNode* __restrict__ bvh;  // per-lane BVH over triangles, or null (batch walk)
     const Bvh4Node* __restrict__ bvh4; // the same BVH collapsed to 4-wide nodes
+    const Bvh4QNode* __restrict__ bvh4q; // ... with quantized child boxes (same node indices)
     const TriGeo* __restrict__ bvh_tris; // BVH-ordered geometry; pad = (triangle, batch, ni)
     const float4* __restrict__ nodes; // batch hierarchy: per node (lo.xyz, -), (hi.xyz, -)
     uint32_t node_off[11];            // first node of level L (L = 1..top) in `nodes`
@@ -155,6 +173,7 @@ struct KArgs {
     SplitCtr* __restrict__ ctr;
     unsigned long long* __restrict__ acc; // per output pixel: fixed-point colour (r, g, b, -)
     uint32_t* __restrict__ spilled;   // output pixels finished by finalize_spilled
+    float4* __restrict__ diag;        // diagnostic builds only (TRT_DIAG_DUMP_SHADOW): ray dump
 };
 
 } // namespace trt

@@ -44,8 +44,16 @@ __device__ __forceinline__ void wave_lds_sync() {
     }
 }
 __device__ __forceinline__ uint32_t lane_id() { return TRT_WPB == 1 ? threadIdx.x : (threadIdx.x & 63u); }
+// Rank of this lane among the set bits of `mask` below it.
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
 
 #define TRT_EPS 0.0001f /* MIN_EPSILON, shader.comp:78 */
+// Shadow queries of lights that add nothing lit or shadowed are not traced (cast_seg).
+#ifndef TRT_SKIP_DARK
+#define TRT_SKIP_DARK 1
+#endif
 #define TRT_PI 3.14159265358979323846f /* PI, shader.comp:82 */
 #define TRT_GAMMA 2.2f /* GAMMA, shader.comp:81 */
 
@@ -145,6 +153,8 @@ struct Cnt {
     // Moller-Trumbore stages reached (the FP32 work units of the VALU roofline):
     // past the parallel test, past the u test, past the v test (t computed)
     uint32_t ta = 0, tu = 0, tv = 0;
+    // shadow queries the frame skips (zero contribution) and the work inside them
+    uint32_t sk = 0, ssph = 0, sbox = 0, stt = 0, sta = 0, stu = 0, stv = 0;
 #ifdef TRT_DIAG_PIXEL_WORK
     uint32_t wn = 0, wt = 0, wseg = 0, wmax = 0; // diagnostic: this lane's node visits, tri tests, segments, max nodes/query
 #endif
@@ -585,6 +595,70 @@ __device__ __forceinline__ bool visit4(f3 o, f3 inv, float best, const float4& l
     return true;
 }
 
+// Quantized 4-wide node (trt_device.h Bvh4QNode): per axis the plane of byte q is p + q * s,
+// so its slab distance is (p - o) * inv + q * (s * inv) = A + q * B, one FMA per plane after
+// three products per axis (the culling test may round freely: the boxes carry a margin of a
+// grid step plus the padding, far above this rounding, so a fused multiply-add is fine here
+// and only here).  The near / far plane of each axis is picked by the sign of inv once per
+// node, so a child needs no per-axis min / max, and an inverted (unused) box is never entered.
+#ifndef TRT_BVH_QUANT
+#define TRT_BVH_QUANT 1
+#endif
+template <bool COUNT, typename Stack>
+__device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& pe, const uint4& qa,
+                                        const uint4& qb, const uint4& ch, Stack& stack, uint32_t& node, Cnt& c) {
+    const uint32_t ex = __float_as_uint(pe.w);
+    const float sx = __uint_as_float((ex & 0xffu) << 23);
+    const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23);
+    const float sz = __uint_as_float(((ex >> 16) & 0xffu) << 23);
+    const float ax = (pe.x - o.x) * inv.x, bx = sx * inv.x;
+    const float ay = (pe.y - o.y) * inv.y, by = sy * inv.y;
+    const float az = (pe.z - o.z) * inv.z, bz = sz * inv.z;
+    // qa = (qlo.x, qlo.y, qlo.z, qhi.x), qb = (qhi.y, qhi.z, -, -)
+    const uint32_t nx = inv.x >= 0.0f ? qa.x : qa.w, fx = inv.x >= 0.0f ? qa.w : qa.x;
+    const uint32_t ny = inv.y >= 0.0f ? qa.y : qb.x, fy = inv.y >= 0.0f ? qb.x : qa.y;
+    const uint32_t nz = inv.z >= 0.0f ? qa.z : qb.y, fz = inv.z >= 0.0f ? qb.y : qa.z;
+    float t[4];
+    uint32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
+    int nh = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int sh = 8 * i;
+        const float tnx = __builtin_fmaf((float)((nx >> sh) & 0xffu), bx, ax);
+        const float tny = __builtin_fmaf((float)((ny >> sh) & 0xffu), by, ay);
+        const float tnz = __builtin_fmaf((float)((nz >> sh) & 0xffu), bz, az);
+        const float tfx = __builtin_fmaf((float)((fx >> sh) & 0xffu), bx, ax);
+        const float tfy = __builtin_fmaf((float)((fy >> sh) & 0xffu), by, ay);
+        const float tfz = __builtin_fmaf((float)((fz >> sh) & 0xffu), bz, az);
+        const float tn = fmaxf(fmaxf(tnx, tny), tnz);
+        const float tf = fminf(fminf(tfx, tfy), tfz);
+        const bool ok = tn <= tf && tf > TRT_EPS && tn <= best;
+        t[i] = ok ? tn : __builtin_huge_valf();
+        nh += ok ? 1 : 0;
+    }
+    if (COUNT) c.nt += (ch.x != kBvh4None) + (ch.y != kBvh4None) + (ch.z != kBvh4None) + (ch.w != kBvh4None);
+    if (nh == 0) return false;
+#define TRT_CSWAP(a, b)                                   \
+    do {                                                  \
+        const bool sw = t[b] < t[a];                      \
+        const float ta = t[a], tb = t[b];                 \
+        const uint32_t ra = r[a], rb = r[b];              \
+        t[a] = sw ? tb : ta;                              \
+        t[b] = sw ? ta : tb;                              \
+        r[a] = sw ? rb : ra;                              \
+        r[b] = sw ? ra : rb;                              \
+    } while (0)
+    TRT_CSWAP(0, 1);
+    TRT_CSWAP(2, 3);
+    TRT_CSWAP(0, 2);
+    TRT_CSWAP(1, 3);
+    TRT_CSWAP(1, 2);
+#undef TRT_CSWAP
+    stack.push_sorted(r, nh);
+    node = r[0];
+    return true;
+}
+
 // 4-wide traversal: the four child boxes of a node in one 128-B fetch, entered nearest first.
 // The root is the same node for every lane: its record is read with wave-uniform (scalar)
 // loads, which the scalar cache serves, instead of a dependent per-lane vector fetch at the
@@ -598,6 +672,44 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
     BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2> stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
+#if TRT_BVH_QUANT
+    // measured: -3 % on C4 (1,600 batches, 4-wave build), +2..3 % on C3 / the shipped frame
+    // (profiles/r02_ab_quant.log), so the quantized nodes serve the 4-wave build only
+    if (GEOM == 3 && A.bvh4q) {
+        {
+            typedef __attribute__((address_space(4))) const float cfloat;
+            typedef __attribute__((address_space(4))) const uint32_t cuint;
+            const cfloat* R = (const cfloat*)(A.bvh4q);
+            const cuint* RC = (const cuint*)(A.bvh4q);
+            const float4 pe = make_float4(R[0], R[1], R[2], R[3]);
+            const uint4 qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+            const uint4 qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+            const uint4 ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
+#ifdef TRT_DIAG_PIXEL_WORK
+            ++c.wn;
+#endif
+            if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) return;
+        }
+        for (;;) {
+            if (!(node & kBvhLeafBit)) {
+                const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
+                const float4 pe = p[0];
+                const uint4 qa = reinterpret_cast<const uint4*>(p)[1];
+                const uint4 qb = reinterpret_cast<const uint4*>(p)[2];
+                const uint4 ch = reinterpret_cast<const uint4*>(p)[3];
+#ifdef TRT_DIAG_PIXEL_WORK
+                ++c.wn;
+#endif
+                if (visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) continue;
+            } else if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
+                occluded = true;
+                return;
+            }
+            if (stack.sp == 0) return;
+            node = stack.pop();
+        }
+    }
+#endif
 #if TRT_ROOT_SCALAR
     {
         // constant address space: the compiler may (and, the address being uniform, does) use
@@ -697,6 +809,19 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
                                                  float4* slab) {
 #ifdef TRT_DIAG_NO_SHADOW
     return false; // diagnostic build only: prices the shadow rays
+#endif
+#ifdef TRT_DIAG_DUMP_SHADOW
+    if (A.diag) { // diagnostic build only: appends the query to A.diag (counters[31]) untraced
+        const uint64_t act = __ballot(true);
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        unsigned long long base = 0;
+        if ((int)lane_id() == leader) base = atomicAdd(&A.counters[31], (unsigned long long)__popcll(act));
+        base = __shfl(base, leader, 64);
+        float4* r = A.diag + 2 * (base + lane_rank(act));
+        r[0] = make_float4(o.x, o.y, o.z, max_dist);
+        r[1] = make_float4(d.x, d.y, d.z, 0.0f);
+        return false;
+    }
 #endif
     if (A.flags & TRT_FLAG_SPHERES) {
 #pragma unroll
@@ -907,9 +1032,6 @@ struct StackOf<CAP, true> {
 
 // ---- subtree split: task queues ------------------------------------------------------------
 
-__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 // Wave-aggregated append of up to two tasks per lane (one atomic per wave).  A task that does
 // not fit the queue is not written and its flag is cleared: the caller traces it in place.
@@ -1041,16 +1163,37 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 f3 ld = normalize3(sub(L, p));
                 float dist = length3(sub(L, p));
                 f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
-                if (COUNT) ++cnt.sh;
-                if (shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab)) continue;
-                float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
-                diffuse = add(diffuse, muls(kdv, diff));
-                f3 rdir = reflect3(neg(ld), n);
+                const float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
+                const f3 rdir = reflect3(neg(ld), n);
 #ifdef TRT_DIAG_NO_POW
-                float spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
+                const float spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
 #else
-                float spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
+                const float spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
 #endif
+                // A light whose diffuse term and specular term both vanish from the colour (a
+                // zero term, or a zero albedo weight: diffuse * 0 = 0 for any finite diffuse)
+                // adds exactly nothing whether it is lit or shadowed, so its shadow query cannot
+                // change the pixel and the frame does not trace it.  The counting pass keeps the
+                // reference's behaviour (traces it and adds the terms when lit: its counters and
+                // image are the reference's, and tests/test_gpu_parity.py checks that its image
+                // equals the frame's bit for bit) and reports the skipped queries and their work.
+                const bool matters = TRT_SKIP_DARK == 0 || (alb[0] != 0.0f && diff != 0.0f) ||
+                                     (alb[1] != 0.0f && spec != 0.0f);
+                if (COUNT) ++cnt.sh;
+                if (!COUNT && !matters) continue;
+                const Cnt before = cnt;
+                const bool occl = shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab);
+                if (COUNT && !matters) {
+                    ++cnt.sk;
+                    cnt.ssph += cnt.sph - before.sph;
+                    cnt.sbox += (cnt.nt + cnt.bt) - (before.nt + before.bt);
+                    cnt.stt += cnt.tt - before.tt;
+                    cnt.sta += cnt.ta - before.ta;
+                    cnt.stu += cnt.tu - before.tu;
+                    cnt.stv += cnt.tv - before.tv;
+                }
+                if (occl) continue;
+                diffuse = add(diffuse, muls(kdv, diff));
                 specular = add(specular, muls(kdv, spec));
             }
             color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
@@ -1292,10 +1435,10 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
 #endif
 
 __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
-    const uint32_t v[13] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt,
-                            cnt.ta, cnt.tu, cnt.tv};
+    const uint32_t v[20] = {cnt.pri, cnt.sec, cnt.sh, cnt.miss, cnt.trin, cnt.sph, cnt.bt, cnt.bh, cnt.tt, cnt.nt,
+                            cnt.ta, cnt.tu, cnt.tv, cnt.sk, cnt.ssph, cnt.sbox, cnt.stt, cnt.sta, cnt.stu, cnt.stv};
 #pragma unroll
-    for (int i = 0; i < 13; ++i) {
+    for (int i = 0; i < 20; ++i) {
         unsigned long long w = wave_sum((unsigned long long)v[i]);
         if (lane_id() == 0) atomicAdd(&A.counters[i], w);
     }
@@ -1422,6 +1565,34 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
                            stream, A);
     }
     hipLaunchKernelGGL(finalize_spilled, dim3(A.num_cus), dim3(256), 0, stream, A);
+}
+
+// Batch of independent shadow queries (any hit, shader.comp:364-399): one lane per query of
+// `rays` (2 float4 each: origin + max distance, direction), 64 consecutive queries per wave;
+// occ[i] = 1 if query i is occluded.  The building block of a deferred-shadow frame and the
+// diagnostic that prices coherent shadow tracing (tools/shadow_exp.py).
+template <int GEOM>
+__global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void shadow_batch_kernel(KArgs A, const float4* __restrict__ rays,
+                                                                                uint32_t n, uint32_t* __restrict__ occ) {
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];
+    Cnt cnt;
+    occ[i] = shadow_intersect<false, GEOM>(A, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), a.w, cnt, slab) ? 1u : 0u;
+}
+
+hipError_t launch_shadow_batch(const KArgs& A0, const float4* rays, uint32_t n, uint32_t* occ, hipStream_t stream) {
+    KArgs A = A0;
+    A.diag = nullptr;
+    const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
+    const dim3 grid((n + 63u) / 64u), block(64);
+    if (!n) return hipSuccess;
+    if (geom == 0) hipLaunchKernelGGL(shadow_batch_kernel<0>, grid, block, 0, stream, A, rays, n, occ);
+    else if (geom == 1) hipLaunchKernelGGL(shadow_batch_kernel<1>, grid, block, 0, stream, A, rays, n, occ);
+    else if (geom == 2) hipLaunchKernelGGL(shadow_batch_kernel<2>, grid, block, 0, stream, A, rays, n, occ);
+    else hipLaunchKernelGGL(shadow_batch_kernel<3>, grid, block, 0, stream, A, rays, n, occ);
+    return hipGetLastError();
 }
 
 // Launch helper: picks the deferred-stack capacity from max_depth (children are made only

@@ -450,16 +450,18 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
         if (p->flags & TRT_FLAG_COUNT) {
             const uint32_t NG = m->nranks * m->groups;
             for (auto& d : m->devs) {
-                uint64_t sum[13] = {0};
+                uint64_t sum[20] = {0};
                 for (uint32_t v = 0; v < m->groups; ++v) {
                     trt_params q = group_params(p, band_rows, NG, d.rank * m->groups + v);
                     q.flags &= ~(TRT_FLAG_DEVICE_PTRS | TRT_FLAG_TIMING);
                     trt_stats s{};
                     MTRY(m, d.ctx, trt_render(d.ctx, &q, nullptr, nullptr, &s));
-                    const uint64_t v13[13] = {s.primary_rays, s.secondary_rays, s.shadow_rays, s.misses, s.tri_nearest,
-                                              s.sphere_tests, s.batch_tests, s.batch_hits, s.tri_tests, s.node_tests,
-                                              s.tri_past_a, s.tri_past_u, s.tri_past_v};
-                    for (int k = 0; k < 13; ++k) sum[k] += v13[k];
+                    const uint64_t vk[20] = {s.primary_rays, s.secondary_rays, s.shadow_rays, s.misses, s.tri_nearest,
+                                             s.sphere_tests, s.batch_tests, s.batch_hits, s.tri_tests, s.node_tests,
+                                             s.tri_past_a, s.tri_past_u, s.tri_past_v, s.shadow_skipped,
+                                             s.skipped_sphere_tests, s.skipped_box_tests, s.skipped_tri_tests,
+                                             s.skipped_tri_past_a, s.skipped_tri_past_u, s.skipped_tri_past_v};
+                    for (int k = 0; k < 20; ++k) sum[k] += vk[k];
                 }
                 MHIP(m, hipSetDevice(d.device));
                 MHIP(m, hipMemcpy(d.scratch, sum, sizeof(sum), hipMemcpyHostToDevice));
@@ -467,10 +469,10 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
             MNCCL(m, ncclGroupStart());
             for (auto& d : m->devs) {
                 MHIP(m, hipSetDevice(d.device));
-                MNCCL(m, ncclAllReduce(d.scratch, d.scratch, 13, ncclUint64, ncclSum, d.comm, d.comm_stream));
+                MNCCL(m, ncclAllReduce(d.scratch, d.scratch, 20, ncclUint64, ncclSum, d.comm, d.comm_stream));
             }
             MNCCL(m, ncclGroupEnd());
-            uint64_t tot[13] = {0};
+            uint64_t tot[20] = {0};
             auto& d0 = m->devs[0];
             MHIP(m, hipSetDevice(d0.device));
             MHIP(m, hipStreamSynchronize(d0.comm_stream));
@@ -492,6 +494,13 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
             st->tri_past_a = tot[10];
             st->tri_past_u = tot[11];
             st->tri_past_v = tot[12];
+            st->shadow_skipped = tot[13];
+            st->skipped_sphere_tests = tot[14];
+            st->skipped_box_tests = tot[15];
+            st->skipped_tri_tests = tot[16];
+            st->skipped_tri_past_a = tot[17];
+            st->skipped_tri_past_u = tot[18];
+            st->skipped_tri_past_v = tot[19];
         }
     }
     return TRT_OK;

@@ -26,7 +26,9 @@
 
 namespace trt {
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
+hipError_t launch_shadow_batch(const KArgs& A, const float4* rays, uint32_t n, uint32_t* occ, hipStream_t stream);
 uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4);
+bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out);
 bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris);
 }
@@ -60,6 +62,7 @@ void free_scene(trt_ctx* c) {
     (void)hipFree(c->d_nodes);
     (void)hipFree(c->d_bvh);
     (void)hipFree(c->d_bvh4);
+    (void)hipFree(c->d_bvh4q);
     (void)hipFree(c->d_bvh_tris);
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade);
@@ -69,6 +72,7 @@ void free_scene(trt_ctx* c) {
     c->d_nodes = nullptr;
     c->d_bvh = nullptr;
     c->d_bvh4 = nullptr;
+    c->d_bvh4q = nullptr;
     c->d_bvh_tris = nullptr;
     c->top = 0;
     c->d_geo = nullptr;
@@ -171,7 +175,7 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipSetDevice(hip_device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 32 * sizeof(unsigned long long)) != hipSuccess) {
         trt_destroy(c);
         return TRT_ERR_HIP;
     }
@@ -400,6 +404,13 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         // the 4-wide walk only when its worst-case stack fits (else the BVH2 walk: <= depth)
         if (trt::collapse_bvh4(bvh, bvh4) > (uint32_t)trt::kBvhStack) bvh4.clear();
         bvh4_n = bvh4.size();
+        std::vector<trt::Bvh4QNode> bvh4q;
+        if (!bvh4.empty() && trt::quantize_bvh4(bvh4, bvh4q) &&
+            (rc = upload((void**)&c->d_bvh4q, bvh4q.data(), sizeof(trt::Bvh4QNode) * bvh4q.size(),
+                         "upload quantized bvh4")) != TRT_OK) {
+            free_scene(c);
+            return rc;
+        }
         if ((rc = upload((void**)&c->d_bvh, bvh.data(), sizeof(trt::BvhNode) * bvh.size(), "upload bvh")) != TRT_OK ||
             (!bvh4.empty() && (rc = upload((void**)&c->d_bvh4, bvh4.data(), sizeof(trt::Bvh4Node) * bvh4.size(),
                                             "upload bvh4")) != TRT_OK) ||
@@ -429,6 +440,7 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         sb[trt::kSceneBvhTris] = sizeof(TriGeo) * bvh_tris.size();
     }
     if (c->d_bvh4) sb[trt::kSceneBvh4] = sizeof(trt::Bvh4Node) * bvh4_n;
+    if (c->d_bvh4q) sb[trt::kSceneBvh4Q] = sizeof(trt::Bvh4QNode) * bvh4_n;
     if (c->d_env) sb[trt::kSceneEnv] = (size_t)env_w * env_h * 4;
     c->nbatch = nmodel;
     c->top = top;
@@ -487,6 +499,8 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.nodes = c->d_nodes;
     A.bvh = c->d_bvh;
     A.bvh4 = c->d_bvh4;
+    A.bvh4q = c->d_bvh4q;
+    A.diag = reinterpret_cast<float4*>(c->diag);
     A.bvh_tris = c->d_bvh_tris;
     A.top = c->top;
     std::memcpy(A.node_off, c->node_off, sizeof(A.node_off));
@@ -712,7 +726,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     }
     const uint32_t slot = render_slot(c, c->stream);
     if ((rc = prepare_split(c, p, A, slot, c->stream)) != TRT_OK) return rc;
-    if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
+    if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 32 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
     if ((rc = fence_split(c, A, slot, c->stream)) != TRT_OK) return rc;
@@ -721,7 +735,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
         HIP_TRY(c, hipMemcpyAsync(out8, c->d_out8, npx * 4, hipMemcpyDeviceToHost, c->stream));
     if (out32 && !dev)
         HIP_TRY(c, hipMemcpyAsync(out32, c->d_out32, npx * 16, hipMemcpyDeviceToHost, c->stream));
-    unsigned long long cnt[16] = {0};
+    unsigned long long cnt[32] = {0};
     if (count)
         HIP_TRY(c, hipMemcpyAsync(cnt, c->d_counters, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     if (!dev || count || timing) HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -739,6 +753,13 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
         st->tri_past_a = cnt[10];
         st->tri_past_u = cnt[11];
         st->tri_past_v = cnt[12];
+        st->shadow_skipped = cnt[13];
+        st->skipped_sphere_tests = cnt[14];
+        st->skipped_box_tests = cnt[15];
+        st->skipped_tri_tests = cnt[16];
+        st->skipped_tri_past_a = cnt[17];
+        st->skipped_tri_past_u = cnt[18];
+        st->skipped_tri_past_v = cnt[19];
         st->kernel_ms = 0.0;
         if (timing) {
             float ms = 0.0f;
@@ -824,6 +845,7 @@ void** scene_buf(trt_ctx* c, int k) {
     case kSceneGeo: return reinterpret_cast<void**>(&c->d_geo);
     case kSceneShade: return reinterpret_cast<void**>(&c->d_shade);
     case kSceneMats: return reinterpret_cast<void**>(&c->d_mats);
+    case kSceneBvh4Q: return reinterpret_cast<void**>(&c->d_bvh4q);
     default: return reinterpret_cast<void**>(&c->d_env);
     }
 }
@@ -870,3 +892,33 @@ int scene_adopt(trt_ctx* c, const SceneHeader& h) {
 }
 
 } // namespace trt
+
+// ---- diagnostics (not part of include/trt/abi.h; tools/shadow_exp.py) ----------------------
+
+// Ray-dump buffer of TRT_DIAG_DUMP_SHADOW builds (device pointer, or NULL).
+extern "C" int trt_diag_set_buffer(trt_ctx* c, void* dev_ptr) {
+    if (!c) return TRT_ERR_INVALID;
+    c->diag = dev_ptr;
+    return TRT_OK;
+}
+
+// counters[k] of the last counting pass (k < 32).
+extern "C" unsigned long long trt_diag_counter(trt_ctx* c, uint32_t k) {
+    unsigned long long v = 0;
+    if (!c || k >= 32 || hipSetDevice(c->device) != hipSuccess) return 0;
+    if (hipMemcpy(&v, c->d_counters + k, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return v;
+}
+
+// Traces n shadow queries (2 float4 each, device) into occ (device, one uint32 each) on the
+// context's stream with the frame params' traversal (BVH build, waves).
+extern "C" int trt_diag_shadow_batch(trt_ctx* c, const trt_params* p, const void* rays, uint32_t n, void* occ) {
+    if (!c) return TRT_ERR_INVALID;
+    int rc = check_params(c, p);
+    if (rc != TRT_OK) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    KArgs A;
+    fill_args(c, p, A);
+    HIP_TRY(c, trt::launch_shadow_batch(A, static_cast<const float4*>(rays), n, static_cast<uint32_t*>(occ), c->stream));
+    return TRT_OK;
+}

@@ -108,11 +108,20 @@ class Stats(ctypes.Structure):
         ("tri_past_a", ctypes.c_uint64),
         ("tri_past_u", ctypes.c_uint64),
         ("tri_past_v", ctypes.c_uint64),
+        ("shadow_skipped", ctypes.c_uint64),
+        ("skipped_sphere_tests", ctypes.c_uint64),
+        ("skipped_box_tests", ctypes.c_uint64),
+        ("skipped_tri_tests", ctypes.c_uint64),
+        ("skipped_tri_past_a", ctypes.c_uint64),
+        ("skipped_tri_past_u", ctypes.c_uint64),
+        ("skipped_tri_past_v", ctypes.c_uint64),
     ]
 
     COUNTERS = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
                 "sphere_tests", "batch_tests", "batch_hits", "tri_tests", "node_tests",
-                "tri_past_a", "tri_past_u", "tri_past_v")
+                "tri_past_a", "tri_past_u", "tri_past_v", "shadow_skipped", "skipped_sphere_tests",
+                "skipped_box_tests", "skipped_tri_tests", "skipped_tri_past_a", "skipped_tri_past_u",
+                "skipped_tri_past_v")
     # counters that must equal the oracle's (the reference's work); batch_tests / node_tests
     # depend on the traversal (the kernel culls with a conservative hierarchy)
     EXACT = ("primary_rays", "secondary_rays", "shadow_rays", "misses", "tri_nearest",
@@ -126,7 +135,7 @@ class Stats(ctypes.Structure):
         return d
 
 
-assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 112
+assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 168
 
 
 def make_params(
