@@ -166,6 +166,29 @@ int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
 #define TRT_SPLIT_OFF 1
 int trt_set_subtree_split(trt_ctx* ctx, int window);
 
+/* Deferred shadow rays (the reference traces a hit's three shadow rays in place inside the
+ * pixel's DFS, shader.comp:483-507).  A deferred frame runs in three passes: (A) every pixel's
+ * Whitted tree without shadow rays, logging one colour event per segment in the reference's
+ * pop order, with the shadow queries appended to one dense queue; (B) the queue traced with
+ * every lane of every wave busy (in the per-pixel loop a wave runs the shadow rays of only the
+ * lanes that sit at a hit); (C) each pixel's events summed in logged order with the shader's
+ * own arithmetic.  The image is bit-identical to the per-pixel loop without subtree split (the
+ * reference's single running sum), rays and counters are unchanged, and a pixel whose log does
+ * not fit the scratch is re-traced in place.  A deferred frame is never split.  COUNT and
+ * spp > 1 frames always run the per-pixel loop.
+ * mode: TRT_DEFER_AUTO (default: mesh scenes with max_depth >= 8, unless a subtree-split
+ * window 2..5 was set explicitly), TRT_DEFER_OFF, TRT_DEFER_ON. */
+#define TRT_DEFER_AUTO 0
+#define TRT_DEFER_OFF 1
+#define TRT_DEFER_ON 2
+int trt_set_deferred_shadows(trt_ctx* ctx, int mode);
+
+/* Counters of the last deferred frame rendered on `slot` (0 .. TRT_MAX_FRAMES_IN_FLIGHT-1;
+ * trt_render uses one slot per stream): out[0] event chunks taken, out[1] shadow queries
+ * appended, out[2] pixels re-traced in place, out[3] chunk capacity, out[4] query capacity.
+ * Waits for the context's stream. */
+int trt_defer_stats(trt_ctx* ctx, uint32_t slot, uint64_t out[5]);
+
 /* The reference's frame loop (mainLoop -> drawFrame, main.cpp:405-438, 2181-2205) in one
  * call: for each of `nframes` frames, updateUniformBuffer with ubos[i] (or the current UBO
  * when ubos is NULL) and enqueue one trace launch writing out_rgba8 + i * frame_stride

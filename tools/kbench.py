@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--inflight", type=int, default=2, help="frames in flight")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (0 auto, 1 off, 2..5)")
+    ap.add_argument("--defer", type=int, default=0, help="deferred shadows (0 auto, 1 off, 2 on)")
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=None, help="override trt_params.flags")
     a = ap.parse_args()
     import numpy as np
@@ -55,6 +56,7 @@ def main():
     r.set_stream(stream)
     r.set_frames_in_flight(a.inflight)
     r.set_subtree_split(a.split)
+    r.set_deferred_shadows(a.defer)
     r.render_frames(p, out, 5)
     r.render_frames(p, out, a.frames, timing=True)
     ms = r.frame_times(a.frames)
@@ -72,11 +74,13 @@ def main():
     torch.cuda.synchronize()
     wall_ev = e0.elapsed_time(e1) / a.frames
     rays = st["primary_rays"] + st["secondary_rays"]
-    res = {"tag": a.tag, "inflight": a.inflight, "split": a.split, "config": a.config,
+    res = {"tag": a.tag, "inflight": a.inflight, "split": a.split, "defer": a.defer, "config": a.config,
            "size": [p.width, p.height], "depth": p.max_depth, "rays": rays,
            "med_us": round(float(np.median(ms)) * 1e3, 2), "min_us": round(float(ms.min()) * 1e3, 2),
            "Mray_s_kernel": round(rays / (float(np.median(ms)) * 1e-3) / 1e6, 1),
            "wall_us_no_events": round(wall_noev * 1e3, 2), "wall_us_events_every16": round(wall_ev * 1e3, 2)}
+    if a.defer != 1:
+        res["defer_stats"] = r.defer_stats(0)
     print(json.dumps(res), flush=True)
     r.close()
 

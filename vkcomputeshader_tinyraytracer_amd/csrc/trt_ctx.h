@@ -47,6 +47,7 @@ struct trt_ctx {
     uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     int subtree_split = TRT_SPLIT_AUTO;
+    int deferred_shadows = TRT_DEFER_AUTO;
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.
@@ -57,6 +58,15 @@ struct trt_ctx {
         trt::SplitCtr* ctr = nullptr;
         size_t npx = 0;  // pixels the buffers hold
         uint32_t cap = 0; // tasks per queue
+        // Deferred-shadow scratch (trt_set_deferred_shadows): event chunks + links, the
+        // shadow query queue, per-pixel log heads, the fallback list and the counters.
+        float4* ev = nullptr;
+        uint32_t* ev_next = nullptr;
+        float4* shq = nullptr;
+        uint2* px_ev = nullptr;
+        uint32_t* fb = nullptr;
+        trt::DeferCtr* dctr = nullptr;
+        size_t ev_chunks = 0, shq_cap = 0, dnpx = 0;
         // The stream of the slot's last frame and an event after it: a frame on another
         // stream waits for it before reusing the scratch (trt_render on alternating
         // streams, e.g. dist.PipelinedTiles, must not race on the task queues).

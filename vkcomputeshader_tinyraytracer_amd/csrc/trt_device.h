@@ -121,6 +121,28 @@ struct SplitCtr {
     uint32_t head[kMaxSplitRounds + 1];     // dequeue head of launch r's output (read by r + 1)
 };
 
+// Deferred-shadow frame (trt_set_deferred_shadows).  Pass A traces every pixel's Whitted tree
+// without its shadow rays and logs, per DFS step, one colour event (in the reference's pop
+// order) into a chunked per-lane log; the shadow queries go to one dense queue that pass B
+// traces with every lane busy; pass C replays each pixel's events in order.  A chunk holds
+// kEvRows events of the 64 lanes of a wave, laid out [row][plane][lane] (4 x 16 B planes per
+// event, coalesced across lanes); ev_next[chunk * 64 + lane] links a lane's chunks.
+constexpr uint32_t kEvRows = 4u;
+constexpr uint32_t kEvNone = 0xFFFFFFFFu;  // px_ev.x of a pixel re-traced by defer_fallback
+constexpr uint32_t kEvConst = 0xFFFFFFFFu; // plane0.w of an event whose colour is known in pass A
+// The event pool and the query queue are split into kDeferStripes stripes (tile t allocates
+// from stripe hash(t), each with its own counter on its own 64-B line): one counter
+// for a whole 4K frame serialises ~10^6 wave-aggregated atomics in one L2 channel (measured:
+// a 4K depth-4 frame 2.5x slower).  Pass B walks the stripes with a static grid, no atomics.
+constexpr uint32_t kDeferStripes = 128u;
+constexpr uint32_t kCtrStride = 16u; // uint32 per counter line
+struct DeferCtr {
+    uint32_t nfb;                                  // pixels handed to defer_fallback
+    uint32_t pad[kCtrStride - 1];
+    uint32_t chunks[kDeferStripes * kCtrStride];   // [s * kCtrStride]: chunks taken from stripe s
+    uint32_t nq[kDeferStripes * kCtrStride];       // [s * kCtrStride]: queries appended to stripe s
+};
+
 struct SphereArg {
     float c[3];
     float r;
@@ -174,6 +196,16 @@ struct KArgs {
     unsigned long long* __restrict__ acc; // per output pixel: fixed-point colour (r, g, b, -)
     uint32_t* __restrict__ spilled;   // output pixels finished by finalize_spilled
     float4* __restrict__ diag;        // diagnostic builds only (TRT_DIAG_DUMP_SHADOW): ray dump
+    // deferred shadows (defer != 0): event log, shadow query queue, per-pixel log heads
+    uint32_t defer;
+    uint32_t ev_cap;                  // event chunks per stripe (stripe s: chunks [s * ev_cap, ...))
+    uint32_t shq_cap;                 // queries per stripe (stripe s: queries [s * shq_cap, ...))
+    float4* __restrict__ ev;          // chunks of kEvRows x 4 planes x 64 lanes float4
+    uint32_t* __restrict__ ev_next;   // per chunk and lane: the lane's next chunk
+    float4* __restrict__ shq;         // per query: (origin, max distance), (direction, slot << 2 | light)
+    uint2* __restrict__ px_ev;        // per output pixel: (first chunk or kEvNone, events)
+    uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
+    DeferCtr* __restrict__ dctr;
 };
 
 } // namespace trt

@@ -1070,16 +1070,67 @@ __device__ __forceinline__ float from_fixed(unsigned long long v) {
     return (float)((double)(long long)v * (1.0 / 4294967296.0));
 }
 
+// ---- deferred shadows: the per-lane event log (trt_device.h kEvRows) ---------------------
+struct EvLog {
+    uint32_t stripe = 0;     // the tile's stripe of the event pool and the query queue
+    uint32_t k = 0;          // events this lane has logged
+    uint32_t chunk = 0;      // the chunk holding event k - 1
+    uint32_t first = kEvNone;
+    bool ovf = false;        // event pool or query queue full: defer_fallback re-traces the pixel
+};
+
+// Slot of this lane's next event; every active lane calls it once per DFS step.  Lanes that
+// start a chunk together share one (wave-aggregated atomic); each lane links its own chain.
+__device__ __forceinline__ uint32_t ev_alloc(const KArgs& A, EvLog& L) {
+    const uint32_t row = L.k % kEvRows;
+    const bool need = row == 0u && !L.ovf;
+    const uint64_t m = __ballot(need);
+    if (m) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if ((int)lane_id() == leader) base = atomicAdd(&A.dctr->chunks[L.stripe * kCtrStride], 1u);
+        base = __shfl(base, leader, 64);
+        if (need) {
+            if (base >= A.ev_cap) {
+                L.ovf = true;
+            } else {
+                base += L.stripe * A.ev_cap;
+                if (L.k == 0u) L.first = base;
+                else A.ev_next[(size_t)L.chunk * 64u + lane_id()] = base;
+                L.chunk = base;
+            }
+        }
+    }
+    ++L.k;
+    return (L.chunk * kEvRows + row) * 64u + lane_id();
+}
+// Plane p (0..3) of event slot s = (chunk * kEvRows + row) * 64 + lane.
+__device__ __forceinline__ float4* ev_plane(const KArgs& A, uint32_t s, uint32_t p) {
+    return A.ev + ((size_t)(s >> 6) * 4u + p) * 64u + (s & 63u);
+}
+
 // The DFS of one segment tree (root = a primary ray, or a task of a split launch).  Returns
 // the unclamped colour sum in the reference's pop order.  SPLIT: children at depth
 // >= A.split_d1 are handed to the task queue (`spilled` is set) instead of being traced.
-template <int CAP, bool COUNT, int GEOM, bool SPLIT>
+// DEFER: no shadow ray is traced and nothing is summed; each step logs its colour event into
+// *elog (a miss's or an unlit hit's colour term, or a hit's Phong terms with the lights whose
+// shadow queries it appended to A.shq) for defer_resolve to sum in this same order.  HYB:
+// the deferred refraction children live in CAP LDS entries plus a private tail.
+template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
 __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float* lds, float4* slab,
-                                       uint32_t pixel, bool& spilled) {
+                                       uint32_t pixel, bool& spilled, EvLog* elog = nullptr) {
+#ifdef TRT_BG_EARLY
+    static_assert(!DEFER, "TRT_BG_EARLY (diagnostic) does not log deferred events");
+#endif
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    typename StackOf<CAP, SPLIT>::type stk(lds);
+    typename StackOf<CAP, HYB>::type stk(lds);
     for (;;) {
+        uint32_t slot = 0;
+        if (DEFER) {
+            slot = ev_alloc(A, *elog);
+            if (elog->ovf) break;
+        }
         if (COUNT && cur.depth > 0) ++cnt.sec;
 #ifdef TRT_DIAG_PIXEL_WORK
         ++cnt.wseg;
@@ -1105,7 +1156,12 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             if (!env_miss) color = add(color, muls(mk(0.2f, 0.7f, 0.8f), cur.thr));
 #else
             f3 bg = background(A, cur.d);
-            color = add(color, muls(bg, cur.thr));
+            if (DEFER) {
+                const f3 c = muls(bg, cur.thr);
+                *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvConst));
+            } else {
+                color = add(color, muls(bg, cur.thr));
+            }
 #endif
         } else {
             // Resolve the closest hit: point, normal, material (shader.comp:302-360).
@@ -1157,6 +1213,8 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             f3 v = neg(cur.d);
             f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
             f3 kdv = mk(kd[0], kd[1], kd[2]);
+            float dterm[3] = {0.0f, 0.0f, 0.0f}, sterm[3] = {0.0f, 0.0f, 0.0f};
+            uint32_t qmask = 0; // DEFER: lights whose shadow query went to A.shq
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
@@ -1181,6 +1239,28 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                                      (alb[1] != 0.0f && spec != 0.0f);
                 if (COUNT) ++cnt.sh;
                 if (!COUNT && !matters) continue;
+                if (DEFER) {
+                    // Append the query (lanes of one light together: neighbouring queries of
+                    // the dense pass-B queue share a light and nearby origins).
+                    const uint64_t m = __ballot(true);
+                    const int leader = __ffsll((unsigned long long)m) - 1;
+                    uint32_t base = 0;
+                    if ((int)lane_id() == leader)
+                        base = atomicAdd(&A.dctr->nq[elog->stripe * kCtrStride], (uint32_t)__popcll(m));
+                    base = __shfl(base, leader, 64);
+                    const uint32_t qi = base + lane_rank(m);
+                    if (qi < A.shq_cap) {
+                        float4* q = A.shq + 2 * ((size_t)elog->stripe * A.shq_cap + qi);
+                        q[0] = make_float4(so.x, so.y, so.z, dist);
+                        q[1] = make_float4(ld.x, ld.y, ld.z, __uint_as_float((slot << 2) | (uint32_t)i));
+                        qmask |= 1u << i;
+                        dterm[i] = diff;
+                        sterm[i] = spec;
+                    } else {
+                        elog->ovf = true;
+                    }
+                    continue;
+                }
                 const Cnt before = cnt;
                 const bool occl = shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab);
                 if (COUNT && !matters) {
@@ -1196,7 +1276,20 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 diffuse = add(diffuse, muls(kdv, diff));
                 specular = add(specular, muls(kdv, spec));
             }
-            color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
+            if (DEFER) {
+                if (elog->ovf) break;
+                if (qmask == 0u) { // no light can add anything: the colour term is known now
+                    const f3 c = muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr);
+                    *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvConst));
+                } else { // pass B ORs the occluded lights into plane 3's second word
+                    *ev_plane(A, slot, 0) = make_float4(kd[0], kd[1], kd[2], __uint_as_float(qmask));
+                    *ev_plane(A, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], alb[0]);
+                    *ev_plane(A, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], alb[1]);
+                    *reinterpret_cast<float2*>(ev_plane(A, slot, 3)) = make_float2(cur.thr, 0.0f);
+                }
+            } else {
+                color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
+            }
             // Children (shader.comp:509-575).  Children that the reference would push and
             // then drop unseen at the depth / throughput test (shader.comp:449) are not made.
             const int cd = cur.depth + 1;
@@ -1343,7 +1436,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
 // One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.  SPLIT
 // (spp == 1 only): a pixel whose tree handed subtrees to the task queue parks its partial
 // colour in A.acc and is finished by finalize_spilled.
-template <int CAP, bool COUNT, int GEOM, bool SPLIT>
+template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
 __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
     const uint32_t lane = lane_id();
     if (tile >= A.ntiles) return;
@@ -1357,6 +1450,27 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     const uint32_t y = band_row(A, k);
     const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
     const size_t o = (size_t)k * A.width + x;
+    if (DEFER) { // pass A of a deferred-shadow frame (spp == 1)
+        EvLog L;
+        // multiplicative hash of the tile: a frame's costly region (a glass object) spans few
+        // tile columns, so tile % stripes would pile its queries into a few stripes
+        L.stripe = (tile * 0x9E3779B1u) >> (32 - 7);
+        static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
+        bool unused = false;
+        cast_seg<CAP, COUNT, GEOM, false, true, HYB>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds, slab,
+                                                     (uint32_t)o, unused, &L);
+        cnt.pri += 1;
+        A.px_ev[o] = make_uint2(L.ovf ? kEvNone : L.first, L.k);
+        const uint64_t fm = __ballot(L.ovf);
+        if (fm) {
+            const int leader = __ffsll((unsigned long long)fm) - 1;
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(&A.dctr->nfb, (uint32_t)__popcll(fm));
+            base = __shfl(base, leader, 64);
+            if (L.ovf) A.fb[base + lane_rank(fm)] = (uint32_t)o;
+        }
+        return;
+    }
     if (SPLIT) {
         bool spilled = false;
         const f3 c = cast_seg<CAP, COUNT, GEOM, true>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds,
@@ -1451,7 +1565,7 @@ constexpr int slab_float4s() {
 template <int GEOM>
 constexpr int waves_per_simd() { return GEOM == 3 ? TRT_G3_WAVES : TRT_WAVES; }
 
-template <int CAP, bool COUNT, int GEOM, bool SPLIT>
+template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
 __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_kernel(KArgs A) {
 #if TRT_WPB > 1
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
@@ -1479,10 +1593,10 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
     // diagnostic: TRT_TPW tiles per wave, grid-strided (b, b + G, ...; G % 8 == 0 keeps XCDs)
     for (uint32_t k = 0; k < TRT_TPW; ++k) {
         const uint32_t b = blockIdx.x + k * gridDim.x;
-        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, b), cnt, lds, slab);
+        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, xcd_tile(A, b), cnt, lds, slab);
     }
 #else
-    trace_tile<CAP, COUNT, GEOM, SPLIT>(A, xcd_tile(A, vb), cnt, lds, slab);
+    trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, xcd_tile(A, vb), cnt, lds, slab);
 #endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
@@ -1567,6 +1681,109 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
     hipLaunchKernelGGL(finalize_spilled, dim3(A.num_cus), dim3(256), 0, stream, A);
 }
 
+// ---- deferred-shadow frame: passes B, C and the fallback ----------------------------------
+//
+// Pass B: the frame's shadow queries (shadow_intersect, shader.comp:364-399; any hit, so their
+// order is free), 64 consecutive queries of one stripe per wave step — every lane of a wave
+// runs a query, where in the per-pixel loop a wave runs the shadow rays of whichever of its
+// lanes sit at a hit.  Static schedule: wave w takes stripe w % kDeferStripes and every
+// (gridDim / kDeferStripes)-th 64-query block of it.  An occluded query ORs its light's bit
+// into its event.
+template <int GEOM>
+__global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArgs A) {
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    Cnt cnt;
+    const uint32_t s = blockIdx.x % kDeferStripes, K = gridDim.x / kDeferStripes;
+    const uint32_t n = min(A.dctr->nq[s * kCtrStride], A.shq_cap);
+    const float4* Q = A.shq + 2 * (size_t)s * A.shq_cap;
+    for (uint32_t base = (blockIdx.x / kDeferStripes) * 64u; base < n; base += K * 64u) {
+        const uint32_t i = base + threadIdx.x;
+        if (i < n) {
+            const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
+            if (shadow_intersect<false, GEOM>(A, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), a.w, cnt, slab)) {
+                const uint32_t t = __float_as_uint(b.w);
+                atomicOr(reinterpret_cast<uint32_t*>(ev_plane(A, t >> 2, 3)) + 1, 1u << (t & 3u));
+            }
+        }
+    }
+}
+
+// Pass C: each pixel's events summed in the order its DFS logged them — the reference's pop
+// order — with exactly cast_seg's arithmetic (a lit light's kd * diffuse / kd * specular terms
+// added in light order, then colour += thr * (diffuse * albedo.x + specular * albedo.y)); then
+// clamp, gamma and the dual store.  Lane = the pixel's lane in its pass-A tile.
+__global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
+    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    if (x >= A.width || k >= A.rows) return;
+    const size_t o = (size_t)k * A.width + x;
+    const uint2 pe = A.px_ev[o];
+    if (pe.x == kEvNone) return; // defer_fallback's pixel
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    uint32_t chunk = pe.x;
+    for (uint32_t j = 0; j < pe.y; ++j) {
+        const uint32_t row = j % kEvRows;
+        if (j != 0u && row == 0u) chunk = A.ev_next[(size_t)chunk * 64u + lane];
+        const uint32_t s = (chunk * kEvRows + row) * 64u + lane;
+        const float4 p0 = *ev_plane(A, s, 0);
+        const uint32_t tag = __float_as_uint(p0.w);
+        if (tag == kEvConst) {
+            color = add(color, mk(p0.x, p0.y, p0.z));
+            continue;
+        }
+        const float4 p1 = *ev_plane(A, s, 1), p2 = *ev_plane(A, s, 2);
+        const float2 p3 = *reinterpret_cast<const float2*>(ev_plane(A, s, 3));
+        const uint32_t lit = tag & ~__float_as_uint(p3.y);
+        const f3 kdv = mk(p0.x, p0.y, p0.z);
+        const float dterm[3] = {p1.x, p1.y, p1.z}, sterm[3] = {p2.x, p2.y, p2.z};
+        f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (!((lit >> i) & 1u)) continue;
+            diffuse = add(diffuse, muls(kdv, dterm[i]));
+            specular = add(specular, muls(kdv, sterm[i]));
+        }
+        color = add(color, muls(add(muls(diffuse, p1.w), muls(specular, p2.w)), p3.x));
+    }
+    store_pixel(A, o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
+}
+
+// Pixels whose log did not fit (event pool or query queue full) are traced again from scratch
+// by the per-pixel loop with in-place shadow rays (persistent waves over the list).
+template <int CAP, int GEOM>
+__global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KArgs A) {
+    __shared__ float lds[lds_stack_floats<CAP>()];
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    Cnt cnt;
+    const uint32_t n = A.dctr->nfb;
+    const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
+    for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+        const uint32_t i = base + threadIdx.x;
+        if (i < n) {
+            const uint32_t o = A.fb[i];
+            const uint32_t k = o / A.width, x = o % A.width;
+            const f3 c = cast_ray<CAP, false, GEOM>(A, orig, primary_dir(A, x, band_row(A, k), 0), cnt, lds, slab);
+            store_pixel(A, o, c);
+        }
+    }
+}
+
+template <int CAP, int GEOM, bool HYB>
+static void launch_defer(const KArgs& A, hipStream_t stream, dim3 grid, dim3 block) {
+    hipLaunchKernelGGL((trace_kernel<CAP, false, GEOM, false, true, HYB>), grid, block, 0, stream, A);
+    // persistent: up to 8 waves per SIMD (the shadow-only kernel is light on VGPRs and LDS;
+    // waves that find the queue drained exit at once)
+    hipLaunchKernelGGL(defer_shadows<GEOM>, dim3(((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes),
+                       dim3(64), 0, stream, A);
+    hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
+    // the fallback runs the per-pixel loop (deep frames: its full-depth private stack)
+    if constexpr (HYB)
+        hipLaunchKernelGGL((defer_fallback<(int)TRT_MAX_DEPTH_LIMIT - 1, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
+    else
+        hipLaunchKernelGGL((defer_fallback<CAP, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
+}
+
 // Batch of independent shadow queries (any hit, shader.comp:364-399): one lane per query of
 // `rays` (2 float4 each: origin + max distance, direction), 64 consecutive queries per wave;
 // occ[i] = 1 if query i is occluded.  The building block of a deferred-shadow frame and the
@@ -1610,6 +1827,25 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const dim3 grid(A.ntiles), block(64);
 #endif
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
+    if (A.defer && !count && A.spp <= 1 && A.dctr && A.ev && A.shq && A.px_ev && A.fb) {
+        hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
+        if (e != hipSuccess) return e;
+#define TRT_DEFER_G(CAP, HYB)                                                \
+    do {                                                                     \
+        if (geom == 0) launch_defer<CAP, 0, HYB>(A, stream, grid, block);    \
+        else if (geom == 1) launch_defer<CAP, 1, HYB>(A, stream, grid, block); \
+        else if (geom == 2) launch_defer<CAP, 2, HYB>(A, stream, grid, block); \
+        else launch_defer<CAP, 3, HYB>(A, stream, grid, block);              \
+    } while (0)
+        // deep trees: 3 deferred children in LDS + a private tail (the split launches' LDS budget)
+        if (D <= 1) TRT_DEFER_G(0, false);
+        else if (D <= 2) TRT_DEFER_G(1, false);
+        else if (D <= 3) TRT_DEFER_G(2, false);
+        else if (D <= 4) TRT_DEFER_G(3, false);
+        else TRT_DEFER_G(3, true);
+#undef TRT_DEFER_G
+        return hipGetLastError();
+    }
     if (A.split_w >= 2 && A.split_w <= 5 && A.split_w < D && A.spp <= 1 && A.acc && A.ctr) {
         hipError_t e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
         if (e != hipSuccess) return e;

@@ -205,6 +205,12 @@ int trt_destroy(trt_ctx* c) {
         (void)hipFree(b.acc);
         (void)hipFree(b.spilled);
         (void)hipFree(b.ctr);
+        (void)hipFree(b.ev);
+        (void)hipFree(b.ev_next);
+        (void)hipFree(b.shq);
+        (void)hipFree(b.px_ev);
+        (void)hipFree(b.fb);
+        (void)hipFree(b.dctr);
         if (b.done) (void)hipEventDestroy(b.done);
     }
     for (hipStream_t s : c->aux) {
@@ -241,6 +247,36 @@ int trt_set_subtree_split(trt_ctx* c, int window) {
     if (window != TRT_SPLIT_AUTO && window != TRT_SPLIT_OFF && (window < 2 || window > 5))
         return fail(c, TRT_ERR_INVALID, "trt_set_subtree_split: window must be 0 (auto), 1 (off) or 2..5");
     c->subtree_split = window;
+    return TRT_OK;
+}
+
+int trt_set_deferred_shadows(trt_ctx* c, int mode) {
+    if (!c) return TRT_ERR_INVALID;
+    if (mode != TRT_DEFER_AUTO && mode != TRT_DEFER_OFF && mode != TRT_DEFER_ON)
+        return fail(c, TRT_ERR_INVALID, "trt_set_deferred_shadows: mode must be TRT_DEFER_AUTO, _OFF or _ON");
+    c->deferred_shadows = mode;
+    return TRT_OK;
+}
+
+int trt_defer_stats(trt_ctx* c, uint32_t slot, uint64_t out[5]) {
+    if (!c || !out) return TRT_ERR_INVALID;
+    if (slot >= TRT_MAX_FRAMES_IN_FLIGHT) return fail(c, TRT_ERR_INVALID, "trt_defer_stats: slot out of range");
+    const auto& b = c->split[slot];
+    for (int i = 0; i < 5; ++i) out[i] = 0;
+    if (!b.dctr) return TRT_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (b.last && b.done) HIP_TRY(c, hipEventSynchronize(b.done));
+    trt::DeferCtr d{};
+    HIP_TRY(c, hipMemcpy(&d, b.dctr, sizeof(d), hipMemcpyDeviceToHost));
+    const size_t ev_s = b.ev_chunks / trt::kDeferStripes, q_s = b.shq_cap / trt::kDeferStripes;
+    for (uint32_t s = 0; s < trt::kDeferStripes; ++s) { // taken = min(requested, stripe capacity)
+        out[0] += std::min<size_t>(d.chunks[s * trt::kCtrStride], ev_s);
+        out[1] += std::min<size_t>(d.nq[s * trt::kCtrStride], q_s);
+    }
+    out[2] = d.nfb;
+    out[3] = b.ev_chunks;
+    out[4] = b.shq_cap;
     return TRT_OK;
 }
 
@@ -531,15 +567,90 @@ uint32_t split_window(const trt_ctx* c, const trt_params* p) {
     return w < D ? w : 0u;
 }
 
-// Allocates slot `slot`'s split scratch for this frame size and fills A's split fields; a
-// frame on `stream` waits for the slot's previous frame when that ran on another stream.
+// Does this frame run deferred shadows?  Auto: mesh scenes with max_depth >= 8, whose deep
+// refraction trees leave most lanes of a wave idle while a few trace their shadow rays.
+// COUNT frames (the reference's counters) and spp > 1 frames run the per-pixel loop; an explicit
+// subtree-split window outranks the automatic choice.
+bool defer_frame(const trt_ctx* c, const trt_params* p) {
+    if (p->spp > 1 || (p->flags & TRT_FLAG_COUNT) || c->deferred_shadows == TRT_DEFER_OFF) return false;
+    if (c->deferred_shadows == TRT_DEFER_ON) return true;
+    const bool split_explicit = c->subtree_split != TRT_SPLIT_AUTO && c->subtree_split != TRT_SPLIT_OFF;
+    return !split_explicit && c->nbatch > 0 && p->max_depth >= 8;
+}
+
+size_t env_cap(const char* name, size_t v) {
+    if (const char* e = std::getenv(name)) return std::min<size_t>(v, (size_t)std::strtoull(e, nullptr, 10));
+    return v;
+}
+
+// Allocates slot `slot`'s deferred-shadow scratch for this frame and fills A's defer fields.
+int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
+    auto& b = c->split[slot];
+    const size_t npx = (size_t)trt_output_rows(p) * p->width;
+    const uint32_t D = p->max_depth;
+    // Event chunks: at depth <= 4 a pixel logs at most 2^D - 1 events (its whole tree), so
+    // ceil((2^D - 1) / kEvRows) chunks per tile never overflow; deeper frames get 4 chunks per
+    // tile on average, at least 128 per stripe (the shipped frame takes 1.3 per tile) (most tiles log one or two events per pixel; a lane that finds the pool
+    // empty is re-traced in place).  Slot ids (chunk * kEvRows + row) * 64 + lane travel in 30
+    // bits of a query.
+    const size_t per_tile = D <= 4 ? ((1u << D) - 1u + trt::kEvRows - 1u) / trt::kEvRows : 4u;
+    // Both are split into kDeferStripes equal stripes (tile t uses stripe hash(t)).
+    constexpr size_t S = trt::kDeferStripes;
+    const size_t tiles_per_stripe = (A.ntiles + S - 1) / S;
+    const size_t chunks = S * std::min<size_t>(std::max<size_t>(tiles_per_stripe * per_tile, D <= 4 ? 16u : 128u),
+                                               (1u << 30) / (trt::kEvRows * 64u) / S);
+    const size_t qcap = S * std::min<size_t>(std::max<size_t>(6 * tiles_per_stripe * 64u, 1u << 12),
+                                             0xFFFFFFFFu / S);
+    if (chunks > b.ev_chunks || qcap > b.shq_cap || npx > b.dnpx) {
+        (void)hipFree(b.ev);
+        (void)hipFree(b.ev_next);
+        (void)hipFree(b.shq);
+        (void)hipFree(b.px_ev);
+        (void)hipFree(b.fb);
+        b.ev = nullptr;
+        b.ev_next = nullptr;
+        b.shq = nullptr;
+        b.px_ev = nullptr;
+        b.fb = nullptr;
+        b.ev_chunks = b.shq_cap = b.dnpx = 0;
+        hipError_t e = hipMalloc((void**)&b.ev, chunks * trt::kEvRows * 4 * 64 * sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.ev_next, chunks * 64 * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.shq, qcap * 2 * sizeof(float4));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.px_ev, npx * sizeof(uint2));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.fb, npx * sizeof(uint32_t));
+        if (e == hipSuccess && !b.dctr) e = hipMalloc((void**)&b.dctr, sizeof(trt::DeferCtr));
+        if (e != hipSuccess) return hip_fail(c, e, "alloc deferred-shadow buffers");
+        b.ev_chunks = chunks;
+        b.shq_cap = qcap;
+        b.dnpx = npx;
+    }
+    A.defer = 1;
+    // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
+    A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", b.ev_chunks / trt::kDeferStripes);
+    A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", b.shq_cap / trt::kDeferStripes);
+    A.ev = b.ev;
+    A.ev_next = b.ev_next;
+    A.shq = b.shq;
+    A.px_ev = b.px_ev;
+    A.fb = b.fb;
+    A.dctr = b.dctr;
+    return TRT_OK;
+}
+
+// Allocates slot `slot`'s split (or deferred-shadow) scratch for this frame size and fills A's
+// split / defer fields; a frame on `stream` waits for the slot's previous frame when that ran
+// on another stream.
 int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipStream_t stream) {
-    A.split_w = split_window(c, p);
+    A.split_w = 0;
     A.split_d1 = A.max_depth;
     A.num_cus = c->num_cus;
-    if (!A.split_w) return TRT_OK;
+    A.defer = 0;
+    const bool defer = defer_frame(c, p);
+    if (!defer) A.split_w = split_window(c, p);
+    if (!A.split_w && !defer) return TRT_OK;
     auto& b = c->split[slot];
     if (b.last && b.last != stream) HIP_TRY(c, hipStreamWaitEvent(stream, b.done, 0));
+    if (defer) return prepare_defer(c, p, A, slot);
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     if (npx > b.npx) {
         // queue capacity: 4 tasks per pixel per window edge (a full queue is not an error: the
@@ -578,7 +689,7 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
 
 // After a split frame's launches on `stream`: the slot's fence.
 int fence_split(trt_ctx* c, const KArgs& A, uint32_t slot, hipStream_t stream) {
-    if (!A.split_w) return TRT_OK;
+    if (!A.split_w && !A.defer) return TRT_OK;
     auto& b = c->split[slot];
     if (!b.done) HIP_TRY(c, hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
     HIP_TRY(c, hipEventRecord(b.done, stream));

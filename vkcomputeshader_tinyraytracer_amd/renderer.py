@@ -65,6 +65,18 @@ class Renderer:
         """trt_set_subtree_split: 0 = auto (default), 1 = off, 2..5 = depth window."""
         self._check(self._L.trt_set_subtree_split(self._h, int(window)))
 
+    def set_deferred_shadows(self, mode: int) -> None:
+        """trt_set_deferred_shadows: 0 = auto (default: mesh scenes at max_depth >= 8), 1 = off,
+        2 = on."""
+        self._check(self._L.trt_set_deferred_shadows(self._h, int(mode)))
+
+    def defer_stats(self, slot: int = 0) -> dict:
+        """trt_defer_stats of in-flight slot `slot` (waits for the context's stream)."""
+        out = (ctypes.c_uint64 * 5)()
+        self._check(self._L.trt_defer_stats(self._h, int(slot), out))
+        return {"chunks": out[0], "queries": out[1], "fallback_pixels": out[2], "chunk_cap": out[3],
+                "query_cap": out[4]}
+
     def set_stream(self, stream) -> None:
         """`stream`: a torch.cuda.Stream (not the legacy default stream), a raw hipStream_t
         int, or None (the context's own stream)."""
