@@ -571,8 +571,9 @@ uint32_t split_window(const trt_ctx* c, const trt_params* p) {
 // refraction trees leave most lanes of a wave idle while a few trace their shadow rays.
 // COUNT frames (the reference's counters) and spp > 1 frames run the per-pixel loop; an explicit
 // subtree-split window outranks the automatic choice.
-bool defer_frame(const trt_ctx* c, const trt_params* p) {
-    if (p->spp > 1 || (p->flags & TRT_FLAG_COUNT) || c->deferred_shadows == TRT_DEFER_OFF) return false;
+bool defer_frame(const trt_ctx* c, const trt_params* p, bool ignore_count = false) {
+    if (p->spp > 1 || c->deferred_shadows == TRT_DEFER_OFF) return false;
+    if ((p->flags & TRT_FLAG_COUNT) && !ignore_count) return false;
     if (c->deferred_shadows == TRT_DEFER_ON) return true;
     const bool split_explicit = c->subtree_split != TRT_SPLIT_AUTO && c->subtree_split != TRT_SPLIT_OFF;
     return !split_explicit && c->nbatch > 0 && p->max_depth >= 8;
@@ -646,7 +647,9 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     A.num_cus = c->num_cus;
     A.defer = 0;
     const bool defer = defer_frame(c, p);
-    if (!defer) A.split_w = split_window(c, p);
+    // A COUNT frame of a scene whose frames run deferred is traced unsplit, so its image is the
+    // deferred frame's bit for bit (both are the reference's single running sum).
+    if (!defer && !defer_frame(c, p, true)) A.split_w = split_window(c, p);
     if (!A.split_w && !defer) return TRT_OK;
     auto& b = c->split[slot];
     if (b.last && b.last != stream) HIP_TRY(c, hipStreamWaitEvent(stream, b.done, 0));
