@@ -174,8 +174,12 @@ int trt_set_subtree_split(trt_ctx* ctx, int window);
  * lanes that sit at a hit); (C) each pixel's events summed in logged order with the shader's
  * own arithmetic.  The image is bit-identical to the per-pixel loop without subtree split (the
  * reference's single running sum), rays and counters are unchanged, and a pixel whose log does
- * not fit the scratch is re-traced in place.  A deferred frame is never split.  COUNT and
- * spp > 1 frames always run the per-pixel loop.
+ * not fit the scratch is re-traced in place.  With an explicit subtree-split window (above) a
+ * deferred frame's subtrees are traced by other lanes into logs of their own, reached through
+ * LINK events at the place of their events, so the sum keeps the reference order (no
+ * fixed-point sums); TRT_SPLIT_AUTO does not split deferred frames.  COUNT and spp > 1 frames
+ * always run the per-pixel loop (a COUNT frame of a scene that would defer runs unsplit, so its
+ * image equals the deferred frame's).
  * mode: TRT_DEFER_AUTO (default: mesh scenes with max_depth >= 8, unless a subtree-split
  * window 2..5 was set explicitly), TRT_DEFER_OFF, TRT_DEFER_ON. */
 #define TRT_DEFER_AUTO 0

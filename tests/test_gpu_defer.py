@@ -66,6 +66,36 @@ def test_deferred_frame_is_bit_identical_to_the_unsplit_loop(gpu_renderer, scene
     assert st["queries"] <= st["query_cap"] and st["chunks"] <= st["chunk_cap"]
 
 
+@pytest.mark.parametrize("name", ["ref", "readme", "c3", "c2d12"])
+@pytest.mark.parametrize("window", [2, 3, 4, 5])
+def test_deferred_split_keeps_the_reference_order(gpu_renderer, scenes, name, window):
+    """Subtree split of a deferred frame: subtrees traced by other lanes log into chains of
+    their own, reached through LINK events at the place of their events: the image is still the
+    unsplit loop's bit for bit (no fixed-point sums)."""
+    sc = scenes[name]
+    if window >= sc.max_depth:
+        pytest.skip("window covers the whole tree: no split")
+    gpu_renderer.upload_scene(sc)
+    d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=window)
+    st = gpu_renderer.defer_stats(0)
+    u8, u32 = _frame(gpu_renderer, sc, DEFER_OFF, split=1)
+    assert st["fallback_pixels"] == 0, st
+    assert np.array_equal(d8, u8) and np.array_equal(d32, u32)
+
+
+def test_deferred_split_task_queue_overflow(gpu_renderer, scenes, monkeypatch):
+    """A task queue far too small: pixels whose subtree does not fit are re-traced in place."""
+    sc = scenes["ref"]
+    gpu_renderer.upload_scene(sc)
+    u8, u32 = _frame(gpu_renderer, sc, DEFER_OFF, split=1)
+    monkeypatch.setenv("TRT_SPLIT_QCAP", "64")
+    d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=2)
+    st = gpu_renderer.defer_stats(0)
+    monkeypatch.delenv("TRT_SPLIT_QCAP")
+    assert st["fallback_pixels"] > 0, st
+    assert np.array_equal(d8, u8) and np.array_equal(d32, u32)
+
+
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 7, 20])
 def test_deferred_depths(gpu_renderer, scenes, depth):
     sc = scenes["c3"]
@@ -97,11 +127,12 @@ def test_overflow_pixels_are_retraced_in_place(gpu_renderer, scenes, monkeypatch
     gpu_renderer.upload_scene(sc)
     u8, u32 = _frame(gpu_renderer, sc, DEFER_OFF)
     monkeypatch.setenv(hook, value)
-    d8, d32 = _frame(gpu_renderer, sc, DEFER_ON)
-    st = gpu_renderer.defer_stats(0)
+    for split in (1, 3):
+        d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=split)
+        st = gpu_renderer.defer_stats(0)
+        assert st["fallback_pixels"] > 0, (split, st)
+        assert np.array_equal(d8, u8) and np.array_equal(d32, u32), split
     monkeypatch.delenv(hook)
-    assert st["fallback_pixels"] > 0, st
-    assert np.array_equal(d8, u8) and np.array_equal(d32, u32)
 
 
 def test_deferred_frames_in_flight(gpu_renderer, scenes):

@@ -32,13 +32,17 @@ def scenes(golden_meshes):
 
 
 def _render(r, sc, window, flags=0):
+    # the fixed-point split of the per-pixel loop (deferred-shadow frames keep the reference
+    # order through LINK events instead: tests/test_gpu_defer.py)
     r.set_subtree_split(window)
+    r.set_deferred_shadows(1)
     try:
         p = sc.params()
         p.flags |= flags
         return r.draw_frame(p, want32=True, count=True)
     finally:
         r.set_subtree_split(0)
+        r.set_deferred_shadows(0)
 
 
 @pytest.mark.parametrize("name", ["ref", "c3", "c2d12"])
@@ -87,11 +91,14 @@ def test_split_queue_overflow_falls_back_in_place(gpu_renderer, scenes, monkeypa
     assert_float_close(g32, o32)
 
 
-def test_split_with_frames_in_flight(gpu_renderer, scenes):
-    """Concurrent split frames use per-slot queues: each equals the single-frame render."""
+@pytest.mark.parametrize("defer", [1, 2])
+def test_split_with_frames_in_flight(gpu_renderer, scenes, defer):
+    """Concurrent split frames use per-slot queues: each equals the single-frame render
+    (per-pixel loop with fixed-point split sums, and deferred shadows with LINK events)."""
     torch = pytest.importorskip("torch")
     sc = scenes["ref"]
     gpu_renderer.upload_scene(sc)
+    gpu_renderer.set_deferred_shadows(defer)
     n, H, W = 5, sc.height, sc.width
     ubos = np.stack([S.make_ubo(cam=(0.03 * i, 0.0, -0.05 * i)) for i in range(n)])
     out = torch.zeros((n, H, W, 4), dtype=torch.uint8, device="cuda")
@@ -109,5 +116,6 @@ def test_split_with_frames_in_flight(gpu_renderer, scenes):
     finally:
         gpu_renderer.set_frames_in_flight(2)
         gpu_renderer.set_subtree_split(0)
+        gpu_renderer.set_deferred_shadows(0)
         gpu_renderer.set_stream(None)
         gpu_renderer.update_ubo(sc.ubo)

@@ -53,6 +53,7 @@ struct trt_ctx {
     // the counters.
     struct SplitBufs {
         trt::Task* q[2] = {nullptr, nullptr};
+        uint32_t* qlink[2] = {nullptr, nullptr}; // deferred split: LINK slot per task
         unsigned long long* acc = nullptr;
         uint32_t* spilled = nullptr;
         trt::SplitCtr* ctr = nullptr;

@@ -130,6 +130,10 @@ struct SplitCtr {
 constexpr uint32_t kEvRows = 4u;
 constexpr uint32_t kEvNone = 0xFFFFFFFFu;  // px_ev.x of a pixel re-traced by defer_fallback
 constexpr uint32_t kEvConst = 0xFFFFFFFFu; // plane0.w of an event whose colour is known in pass A
+// plane0.w of a LINK event (deferred frames with a subtree split): "here come the events of a
+// subtree traced by another lane", plane0 = (first chunk, events, lane, kEvLink) of its chain.
+constexpr uint32_t kEvLink = 0xFFFFFFFEu;
+constexpr uint32_t kMaxLinkDepth = 10u; // nested subtree chains: max_depth / window <= 20 / 2
 // The event pool and the query queue are split into kDeferStripes stripes (tile t allocates
 // from stripe hash(t), each with its own counter on its own 64-B line): one counter
 // for a whole 4K frame serialises ~10^6 wave-aggregated atomics in one L2 channel (measured:
@@ -189,6 +193,9 @@ struct KArgs {
     Task* __restrict__ q_out;         // tasks this launch produces
     const Task* __restrict__ q_in;    // tasks this launch consumes (trace_tasks)
     Task* __restrict__ q_buf[2];      // the two queues of the slot (ping-pong)
+    uint32_t* __restrict__ q_link_out; // deferred split: per task of q_out, its LINK event slot
+    const uint32_t* __restrict__ q_link_in;
+    uint32_t* __restrict__ q_link_buf[2];
     uint32_t* __restrict__ q_out_n;   // produced count of q_out
     const uint32_t* __restrict__ q_in_n;
     uint32_t* __restrict__ q_in_head;

@@ -1035,8 +1035,10 @@ struct StackOf<CAP, true> {
 
 // Wave-aggregated append of up to two tasks per lane (one atomic per wave).  A task that does
 // not fit the queue is not written and its flag is cleared: the caller traces it in place.
+// DEFER: each task also carries the LINK event slot (la / lb) its chain head goes to.
+template <bool DEFER = false>
 __device__ __forceinline__ void enqueue2(const KArgs& A, bool& sa, const Seg& a, bool& sb, const Seg& b,
-                                         uint32_t pixel) {
+                                         uint32_t pixel, uint32_t la = 0, uint32_t lb = 0) {
     const uint64_t ba = __ballot(sa), bb = __ballot(sb);
     if ((ba | bb) == 0ull) return;
     const uint32_t na = (uint32_t)__popcll(ba), nb = (uint32_t)__popcll(bb);
@@ -1046,7 +1048,7 @@ __device__ __forceinline__ void enqueue2(const KArgs& A, bool& sa, const Seg& a,
     if ((int)lane_id() == leader) base = atomicAdd(A.q_out_n, na + nb);
     base = __shfl(base, leader, 64);
     const uint32_t ia = base + lane_rank(ba), ib = base + na + lane_rank(bb);
-    auto put = [&](bool& f, uint32_t i, const Seg& x) {
+    auto put = [&](bool& f, uint32_t i, const Seg& x, uint32_t link) {
         if (!f) return;
         if (i >= A.q_cap) {
             f = false;
@@ -1056,9 +1058,10 @@ __device__ __forceinline__ void enqueue2(const KArgs& A, bool& sa, const Seg& a,
         float4* q = reinterpret_cast<float4*>(A.q_out + i);
         q[0] = make_float4(x.o.x, x.o.y, x.o.z, x.d.x);
         q[1] = make_float4(x.d.y, x.d.z, x.thr, __uint_as_float((pixel << kTaskDepthBits) | (uint32_t)x.depth));
+        if (DEFER) A.q_link_out[i] = link;
     };
-    put(sa, ia, a);
-    put(sb, ib, b);
+    put(sa, ia, a, la);
+    put(sb, ib, b, lb);
 }
 
 // Colours of split pixels are summed in 32.32 fixed point (integer adds: the same result in
@@ -1072,7 +1075,7 @@ __device__ __forceinline__ float from_fixed(unsigned long long v) {
 
 // ---- deferred shadows: the per-lane event log (trt_device.h kEvRows) ---------------------
 struct EvLog {
-    uint32_t stripe = 0;     // the tile's stripe of the event pool and the query queue
+    uint32_t stripe = 0;     // the stripe of the event pool and query queue (wave-uniform)
     uint32_t k = 0;          // events this lane has logged
     uint32_t chunk = 0;      // the chunk holding event k - 1
     uint32_t first = kEvNone;
@@ -1316,7 +1319,22 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 float tt = (refl.thr * refl.thr + refl.thr * refl.thr) + refl.thr * refl.thr;
                 mk_refl = cd < D && !(tt < 0.001f);
             }
-            if (SPLIT && cd >= (int)A.split_d1) { // window edge: both children become tasks
+            if (SPLIT && DEFER && cd >= (int)A.split_d1) {
+                // window edge of a deferred frame: both children become tasks, and this lane's
+                // log gets a LINK event per task at the place of the child's events (reflection
+                // subtree first, as the reference pops it first)
+                bool sa = mk_refl, sb = mk_refr;
+                uint32_t la = 0, lb = 0;
+                if (sa) la = ev_alloc(A, *elog);
+                if (sb) lb = ev_alloc(A, *elog);
+                if (elog->ovf) break;
+                enqueue2<true>(A, sa, refl, sb, refr, pixel, la, lb);
+                if (sa != mk_refl || sb != mk_refr) { // task queue full: re-trace the pixel
+                    elog->ovf = true;
+                    break;
+                }
+                mk_refl = mk_refr = false;
+            } else if (SPLIT && cd >= (int)A.split_d1) { // window edge: both children become tasks
                 bool sa = mk_refl, sb = mk_refr;
                 enqueue2(A, sa, refl, sb, refr, pixel);
                 if (sa) mk_refl = false;
@@ -1457,7 +1475,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
         L.stripe = (tile * 0x9E3779B1u) >> (32 - 7);
         static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
         bool unused = false;
-        cast_seg<CAP, COUNT, GEOM, false, true, HYB>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds, slab,
+        cast_seg<CAP, COUNT, GEOM, SPLIT, true, HYB>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds, slab,
                                                      (uint32_t)o, unused, &L);
         cnt.pri += 1;
         A.px_ev[o] = make_uint2(L.ovf ? kEvNone : L.first, L.k);
@@ -1618,7 +1636,11 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
 // from the previous launch's queue, trace each task's subtree within the depth window (its
 // window-edge children go to the next queue) and add the subtree's colour to its pixel's
 // fixed-point sum.  Every wave leaves once the queue is drained.
-template <int CAP, bool COUNT, int GEOM>
+//
+// DEFER: a task logs its subtree's events into a chain of its own and writes the chain's head
+// into the LINK event its parent logged; a task whose log does not fit hands its pixel to
+// defer_fallback (the pixel's whole tree is re-traced; its other chains are then unused).
+template <int CAP, bool COUNT, int GEOM, bool DEFER = false>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
@@ -1637,6 +1659,19 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
             const uint32_t pixel = pd >> kTaskDepthBits;
             const Seg root{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z, (int)(pd & ((1u << kTaskDepthBits) - 1u))};
             bool spilled = false;
+            if (DEFER) {
+                EvLog L;
+                // wave-uniform (ev_alloc and the query appends reserve from the stripe of the
+                // wave's leader for every lane of the wave)
+                L.stripe = ((base / 64u + 0x5bd1e995u * A.split_d1) * 0x9E3779B1u) >> (32 - 7);
+                cast_seg<CAP, false, GEOM, true, true, true>(A, root, cnt, lds, slab, pixel, spilled, &L);
+                *ev_plane(A, A.q_link_in[t], 0) = make_float4(__uint_as_float(L.first), __uint_as_float(L.k),
+                                                              __uint_as_float(lane_id()), __uint_as_float(kEvLink));
+                // the first chain of a pixel to overflow lists it (pass A lists its own)
+                if (L.ovf && atomicExch(reinterpret_cast<uint32_t*>(A.px_ev + pixel), kEvNone) != kEvNone)
+                    A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pixel;
+                continue;
+            }
             const f3 c = cast_seg<CAP, COUNT, GEOM, true>(A, root, cnt, lds, slab, pixel, spilled);
             unsigned long long* acc = A.acc + 4 * (size_t)pixel;
             atomicAdd(acc + 0, to_fixed(c.x));
@@ -1721,15 +1756,39 @@ __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
     const uint2 pe = A.px_ev[o];
     if (pe.x == kEvNone) return; // defer_fallback's pixel
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    uint32_t chunk = pe.x;
-    for (uint32_t j = 0; j < pe.y; ++j) {
+    // the chain being read: (chunk, lane column, next event, events); LINK events descend into
+    // a subtree's chain (split frames), its end returns to the parent's
+    uint32_t chunk = pe.x, col = lane, j = 0, n = pe.y, sp = 0, steps = 0;
+    uint4 stk[kMaxLinkDepth];
+    for (;;) {
+        if (++steps > 65536u) { // a corrupt log must not hang the GPU: flag it, paint the pixel
+            if (atomicCAS(&A.dctr->pad[0], 0u, 1u) == 0u) {
+                uint32_t* d = A.dctr->pad;
+                d[1] = (uint32_t)o; d[2] = pe.x; d[3] = pe.y; d[4] = chunk; d[5] = col; d[6] = j; d[7] = n; d[8] = sp;
+                for (uint32_t q = 0; q < sp && q < 2u; ++q) { d[9 + 3 * q] = stk[q].x; d[10 + 3 * q] = stk[q].z; d[11 + 3 * q] = stk[q].w; }
+            }
+            color = mk(1.0f, 0.0f, 1.0f);
+            break;
+        }
+        if (j == n) {
+            if (sp == 0u) break;
+            const uint4 f = stk[--sp];
+            chunk = f.x, col = f.y, j = f.z, n = f.w;
+            continue;
+        }
         const uint32_t row = j % kEvRows;
-        if (j != 0u && row == 0u) chunk = A.ev_next[(size_t)chunk * 64u + lane];
-        const uint32_t s = (chunk * kEvRows + row) * 64u + lane;
+        if (j != 0u && row == 0u) chunk = A.ev_next[(size_t)chunk * 64u + col];
+        ++j;
+        const uint32_t s = (chunk * kEvRows + row) * 64u + col;
         const float4 p0 = *ev_plane(A, s, 0);
         const uint32_t tag = __float_as_uint(p0.w);
         if (tag == kEvConst) {
             color = add(color, mk(p0.x, p0.y, p0.z));
+            continue;
+        }
+        if (tag == kEvLink) {
+            if (sp < kMaxLinkDepth) stk[sp++] = make_uint4(chunk, col, j, n);
+            chunk = __float_as_uint(p0.x), col = __float_as_uint(p0.z), j = 0, n = __float_as_uint(p0.y);
             continue;
         }
         const float4 p1 = *ev_plane(A, s, 1), p2 = *ev_plane(A, s, 2);
@@ -1769,14 +1828,46 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KAr
     }
 }
 
+static uint32_t defer_stages() { // debug: TRT_DEFER_STAGES bitmask of passes to launch
+    const char* e = getenv("TRT_DEFER_STAGES");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : 0xFFu;
+}
+
 template <int CAP, int GEOM, bool HYB>
-static void launch_defer(const KArgs& A, hipStream_t stream, dim3 grid, dim3 block) {
-    hipLaunchKernelGGL((trace_kernel<CAP, false, GEOM, false, true, HYB>), grid, block, 0, stream, A);
+static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 block) {
+    KArgs A = A0;
+    const uint32_t stages = defer_stages();
+    const uint32_t D = A.max_depth, W = A.split_w;
+    if (HYB && W >= 2 && W < D && A.ctr && A.q_link_buf[0]) {
+        // subtree split: the tile kernel traces depths < W, each round the next window
+        A.split_d1 = W;
+        A.q_out = A.q_buf[0];
+        A.q_link_out = A.q_link_buf[0];
+        A.q_out_n = &A.ctr->produced[0];
+        if (stages & 1) hipLaunchKernelGGL((trace_kernel<CAP, false, GEOM, true, true, true>), grid, block, 0, stream, A);
+        uint32_t r = 1;
+        for (uint32_t d0 = W; d0 < D && r <= kMaxSplitRounds && (stages & 2); d0 += W, ++r) {
+            A.split_d1 = d0 + W;
+            A.q_in = A.q_buf[(r - 1) & 1];
+            A.q_link_in = A.q_link_buf[(r - 1) & 1];
+            A.q_in_n = &A.ctr->produced[r - 1];
+            A.q_in_head = &A.ctr->head[r - 1];
+            A.q_out = A.q_buf[r & 1];
+            A.q_link_out = A.q_link_buf[r & 1];
+            A.q_out_n = &A.ctr->produced[r];
+            hipLaunchKernelGGL((trace_tasks<CAP, false, GEOM, true>), dim3(A.num_cus * (GEOM == 3 ? 4 * TRT_G3_WAVES : 12)),
+                               dim3(64), 0, stream, A);
+        }
+    } else {
+        hipLaunchKernelGGL((trace_kernel<CAP, false, GEOM, false, true, HYB>), grid, block, 0, stream, A);
+    }
     // persistent: up to 8 waves per SIMD (the shadow-only kernel is light on VGPRs and LDS;
     // waves that find the queue drained exit at once)
-    hipLaunchKernelGGL(defer_shadows<GEOM>, dim3(((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes),
-                       dim3(64), 0, stream, A);
-    hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
+    if (stages & 4)
+        hipLaunchKernelGGL(defer_shadows<GEOM>, dim3(((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes),
+                           dim3(64), 0, stream, A);
+    if (stages & 8) hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
+    if (!(stages & 16)) return;
     // the fallback runs the per-pixel loop (deep frames: its full-depth private stack)
     if constexpr (HYB)
         hipLaunchKernelGGL((defer_fallback<(int)TRT_MAX_DEPTH_LIMIT - 1, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
@@ -1829,6 +1920,7 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
     if (A.defer && !count && A.spp <= 1 && A.dctr && A.ev && A.shq && A.px_ev && A.fb) {
         hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
+        if (e == hipSuccess && A.split_w >= 2 && A.ctr) e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
         if (e != hipSuccess) return e;
 #define TRT_DEFER_G(CAP, HYB)                                                \
     do {                                                                     \

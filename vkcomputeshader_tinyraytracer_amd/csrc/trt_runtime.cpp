@@ -202,6 +202,8 @@ int trt_destroy(trt_ctx* c) {
     for (auto& b : c->split) {
         (void)hipFree(b.q[0]);
         (void)hipFree(b.q[1]);
+        (void)hipFree(b.qlink[0]);
+        (void)hipFree(b.qlink[1]);
         (void)hipFree(b.acc);
         (void)hipFree(b.spilled);
         (void)hipFree(b.ctr);
@@ -549,6 +551,16 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : (c->nbatch >= 1024u ? 1u : 0u);
 }
 
+// Does this frame run deferred shadows?  Auto: mesh scenes with max_depth >= 8, whose deep
+// refraction trees leave most lanes of a wave idle while a few trace their shadow rays.
+// COUNT frames (the reference's counters) and spp > 1 frames run the per-pixel loop.
+bool defer_frame(const trt_ctx* c, const trt_params* p, bool ignore_count = false) {
+    if (p->spp > 1 || c->deferred_shadows == TRT_DEFER_OFF) return false;
+    if ((p->flags & TRT_FLAG_COUNT) && !ignore_count) return false;
+    if (c->deferred_shadows == TRT_DEFER_ON) return true;
+    return c->nbatch > 0 && p->max_depth >= 8;
+}
+
 // The subtree-split window of a frame: 0 = off.  Auto: scenes with meshes (whose deep
 // refraction trees make a few tiles run for milliseconds) with max_depth above the window.
 uint32_t split_window(const trt_ctx* c, const trt_params* p) {
@@ -558,25 +570,16 @@ uint32_t split_window(const trt_ctx* c, const trt_params* p) {
     uint32_t w;
     if (c->subtree_split == TRT_SPLIT_AUTO) {
         // measured (profiles/r01_split_sweep.log): -10..-16 % on the shipped depth-20 frame with
-        // w = 4; +0..+25 % on depth-4 mesh frames (C3/C4) for any window, so only deep trees
-        if (c->nbatch == 0 || D < 8) return 0;
+        // w = 4; +0..+25 % on depth-4 mesh frames (C3/C4) for any window, so only deep trees.
+        // Deferred-shadow frames are not split: their trees hold no shadow rays, and a split
+        // (exact, through LINK events) measured +11..+29 % on the shipped frame and +38..+69 %
+        // on the README scene for windows 2..5 (profiles/r02_ab_defer_split.log).
+        if (c->nbatch == 0 || D < 8 || defer_frame(c, p)) return 0;
         w = 4u;
     } else {
         w = (uint32_t)c->subtree_split;
     }
     return w < D ? w : 0u;
-}
-
-// Does this frame run deferred shadows?  Auto: mesh scenes with max_depth >= 8, whose deep
-// refraction trees leave most lanes of a wave idle while a few trace their shadow rays.
-// COUNT frames (the reference's counters) and spp > 1 frames run the per-pixel loop; an explicit
-// subtree-split window outranks the automatic choice.
-bool defer_frame(const trt_ctx* c, const trt_params* p, bool ignore_count = false) {
-    if (p->spp > 1 || c->deferred_shadows == TRT_DEFER_OFF) return false;
-    if ((p->flags & TRT_FLAG_COUNT) && !ignore_count) return false;
-    if (c->deferred_shadows == TRT_DEFER_ON) return true;
-    const bool split_explicit = c->subtree_split != TRT_SPLIT_AUTO && c->subtree_split != TRT_SPLIT_OFF;
-    return !split_explicit && c->nbatch > 0 && p->max_depth >= 8;
 }
 
 size_t env_cap(const char* name, size_t v) {
@@ -648,37 +651,50 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     A.defer = 0;
     const bool defer = defer_frame(c, p);
     // A COUNT frame of a scene whose frames run deferred is traced unsplit, so its image is the
-    // deferred frame's bit for bit (both are the reference's single running sum).
-    if (!defer && !defer_frame(c, p, true)) A.split_w = split_window(c, p);
+    // deferred frame's bit for bit (both are the reference's single running sum; a deferred
+    // frame's subtree split keeps that order through LINK events).
+    if (defer || !defer_frame(c, p, true)) A.split_w = split_window(c, p);
     if (!A.split_w && !defer) return TRT_OK;
     auto& b = c->split[slot];
     if (b.last && b.last != stream) HIP_TRY(c, hipStreamWaitEvent(stream, b.done, 0));
-    if (defer) return prepare_defer(c, p, A, slot);
+    if (defer) {
+        const int rc = prepare_defer(c, p, A, slot);
+        if (rc != TRT_OK) return rc;
+    }
+    if (!A.split_w) return TRT_OK;
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     if (npx > b.npx) {
         // queue capacity: 4 tasks per pixel per window edge (a full queue is not an error: the
-        // child is traced in place, SplitCtr::overflow counts it)
+        // child is traced in place, SplitCtr::overflow counts it; a deferred frame re-traces
+        // the pixel in place)
         const size_t cap = std::min<size_t>(std::max<size_t>(4 * npx, 1u << 16), 1u << 28);
-        for (auto* q : b.q) (void)hipFree(q);
-        (void)hipFree(b.acc);
-        (void)hipFree(b.spilled);
-        b = {};
+        auto drop = [&] {
+            for (auto*& q : b.q) (void)hipFree(q), q = nullptr;
+            for (auto*& q : b.qlink) (void)hipFree(q), q = nullptr;
+            (void)hipFree(b.acc);
+            (void)hipFree(b.spilled);
+            b.acc = nullptr;
+            b.spilled = nullptr;
+            b.npx = 0;
+            b.cap = 0;
+        };
+        drop();
         hipError_t e = hipMalloc((void**)&b.q[0], cap * sizeof(trt::Task));
         if (e == hipSuccess) e = hipMalloc((void**)&b.q[1], cap * sizeof(trt::Task));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.qlink[0], cap * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.qlink[1], cap * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMalloc((void**)&b.acc, npx * 4 * sizeof(unsigned long long));
         if (e == hipSuccess) e = hipMalloc((void**)&b.spilled, npx * sizeof(uint32_t));
         if (e == hipSuccess && !b.ctr) e = hipMalloc((void**)&b.ctr, sizeof(trt::SplitCtr));
         if (e != hipSuccess) {
-            for (auto* q : b.q) (void)hipFree(q);
-            (void)hipFree(b.acc);
-            (void)hipFree(b.spilled);
-            (void)hipFree(b.ctr);
-            b = {};
+            drop();
             return hip_fail(c, e, "alloc subtree-split buffers");
         }
         b.npx = npx;
         b.cap = (uint32_t)cap;
     }
+    A.q_link_buf[0] = b.qlink[0];
+    A.q_link_buf[1] = b.qlink[1];
     A.q_buf[0] = b.q[0];
     A.q_buf[1] = b.q[1];
     A.q_cap = b.cap;
@@ -1010,6 +1026,15 @@ int scene_adopt(trt_ctx* c, const SceneHeader& h) {
 // ---- diagnostics (not part of include/trt/abi.h; tools/shadow_exp.py) ----------------------
 
 // Ray-dump buffer of TRT_DIAG_DUMP_SHADOW builds (device pointer, or NULL).
+// diagnostic: the first 16 words of slot `slot`'s deferred-frame counters (nfb + pad, where
+// defer_resolve records a log it could not finish)
+extern "C" int trt_diag_defer_pad(trt_ctx* c, uint32_t slot, uint32_t* out16) {
+    if (!c || !out16 || slot >= TRT_MAX_FRAMES_IN_FLIGHT || !c->split[slot].dctr) return TRT_ERR_INVALID;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(out16, c->split[slot].dctr, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return TRT_OK;
+}
+
 extern "C" int trt_diag_set_buffer(trt_ctx* c, void* dev_ptr) {
     if (!c) return TRT_ERR_INVALID;
     c->diag = dev_ptr;
