@@ -35,6 +35,14 @@ def lib() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback"
         )
+    # PyTorch-ROCm bundles its own HIP runtime (ROCm 7.0) while libtrt.so is linked against
+    # /opt/rocm's (7.2, same SONAME).  Measured on the box: when libtrt has initialised HIP
+    # before torch is imported, torch's device init fails ("No HIP GPUs are available"); with
+    # torch imported first both work.  So when torch is importable it is loaded first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(os.fspath(LIB_PATH))
     c_int, c_u32, vp = ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p
     f3 = ctypes.POINTER(ctypes.c_float)

@@ -32,6 +32,11 @@ struct trt_ctx {
     trt::TriShade* d_shade = nullptr;
     trt::Mat* d_mats = nullptr;
     uint32_t* d_env = nullptr;
+    // envmap footprint layout derived from d_env (trt_kernel.hip env_fetch): (H + 2) x (W + 3)
+    // texel pairs, rebuilt lazily before the first render after d_env changes
+    uint2* d_envp = nullptr;
+    size_t envp_cap = 0;
+    bool envp_ok = false;
     uint32_t nbatch = 0, ntri = 0, nmat = 0, env_w = 0, env_h = 0;
 
     void* d_out8 = nullptr;

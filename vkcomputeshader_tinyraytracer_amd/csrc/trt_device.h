@@ -170,6 +170,10 @@ struct KArgs {
     const TriShade* __restrict__ shade;
     const Mat* __restrict__ mats;
     const uint32_t* __restrict__ env; // RGBA8 texels
+    // Pair rows: entry (r, c) of (env_h + 2) x (env_w + 3) is the texels (x, y0), (x, y1) with
+    // x = clamp(c - 1), y0 = clamp(r - 1), y1 = clamp(r): a bilinear footprint is the 16 bytes at
+    // (yf + 1, xf + 1) — one load (clamp-to-edge included) instead of two rows' lines.
+    const uint2* __restrict__ envp;
     uint32_t env_w, env_h;
     const float* __restrict__ rays_in; // Ray records (8 floats), or null
     uint32_t* __restrict__ out8;       // packed RGBA8, or null

@@ -856,6 +856,9 @@ __device__ __forceinline__ float unorm8(uint32_t c) {
     return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
+#ifndef TRT_ENV_PAIRROWS
+#define TRT_ENV_PAIRROWS 1
+#endif
 #ifndef TRT_ENV_PAIRS
 #define TRT_ENV_PAIRS 1
 #endif
@@ -895,6 +898,22 @@ __device__ __forceinline__ EnvFetch env_fetch(const KArgs& A, f3 d) {
     ix0 = min(max(ix0, 0), W - 1);
     iy0 = min(max(iy0, 0), H - 1);
     EnvFetch e;
+#if TRT_ENV_PAIRROWS
+    if (A.envp) {
+        // ix0 - ix1 and iy0 - iy1 as below: column xf + 1 and row yf + 1 of the pair rows
+        const int c = (int)fminf(fmaxf(xf, -1.0f), (float)W) + 1;
+        const int r = (int)fminf(fmaxf(yf, -1.0f), (float)H) + 1;
+        uint4 q;
+        __builtin_memcpy(&q, A.envp + ((uint32_t)r * (uint32_t)(W + 3) + (uint32_t)c), sizeof(q));
+        e.c00 = q.x;
+        e.c01 = q.y;
+        e.c10 = q.z;
+        e.c11 = q.w;
+        e.a = a;
+        e.b = b;
+        return e;
+    }
+#endif
 #if TRT_ENV_PAIRS
     if (W >= 2) {
         // Each row's two texels in one 8-byte load at base = min(ix0, W - 2): the footprint is
@@ -1984,6 +2003,27 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     else TRT_LAUNCH(19);
 #undef TRT_LAUNCH
 #undef TRT_LAUNCH_G
+    return hipGetLastError();
+}
+
+} // namespace trt
+
+// ---- envmap pair rows (KArgs::envp) --------------------------------------------------------
+namespace trt {
+
+__global__ __launch_bounds__(256) void envp_kernel(const uint32_t* __restrict__ env, uint2* __restrict__ out,
+                                                   uint32_t W, uint32_t H) {
+    const uint32_t r = blockIdx.y, pw = W + 3u;
+    const uint32_t y0 = r == 0u ? 0u : min(r - 1u, H - 1u), y1 = min(r, H - 1u);
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < pw; c += gridDim.x * blockDim.x) {
+        const uint32_t x = c == 0u ? 0u : min(c - 1u, W - 1u);
+        out[(size_t)r * pw + c] = make_uint2(env[(size_t)y0 * W + x], env[(size_t)y1 * W + x]);
+    }
+}
+
+hipError_t launch_envp(const uint32_t* env, uint2* out, uint32_t W, uint32_t H, hipStream_t stream) {
+    if (!W || !H) return hipSuccess;
+    hipLaunchKernelGGL(envp_kernel, dim3((W + 3u + 255u) / 256u, H + 2u), dim3(256), 0, stream, env, out, W, H);
     return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@
 
 namespace trt {
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
+hipError_t launch_envp(const uint32_t* env, uint2* out, uint32_t W, uint32_t H, hipStream_t stream);
 hipError_t launch_shadow_batch(const KArgs& A, const float4* rays, uint32_t n, uint32_t* occ, hipStream_t stream);
 uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4);
 bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out);
@@ -79,6 +80,7 @@ void free_scene(trt_ctx* c) {
     c->d_shade = nullptr;
     c->d_mats = nullptr;
     c->d_env = nullptr;
+    c->envp_ok = false;
     c->nbatch = c->ntri = c->nmat = c->env_w = c->env_h = 0;
     std::memset(c->scene_bytes, 0, sizeof(c->scene_bytes));
     c->have_scene = false;
@@ -194,6 +196,7 @@ int trt_destroy(trt_ctx* c) {
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     free_scene(c);
+    (void)hipFree(c->d_envp);
     (void)hipFree(c->d_out8);
     (void)hipFree(c->d_out32);
     (void)hipFree(c->d_rays);
@@ -494,6 +497,26 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
 
 namespace {
 
+// Builds the envmap pair rows (KArgs::envp) on `stream` when d_env changed since the last
+// build.  Without them (TRT_ENV_PAIRROWS=0 in the environment) env_fetch reads d_env directly.
+int ensure_envp(trt_ctx* c, const trt_params* p, hipStream_t stream) {
+    if (!(p->flags & TRT_FLAG_ENVMAP) || !c->d_env || c->envp_ok) return TRT_OK;
+    if (const char* e = std::getenv("TRT_ENV_PAIRROWS"))
+        if (std::atoi(e) == 0) return TRT_OK;
+    const size_t bytes = ((size_t)c->env_h + 2) * ((size_t)c->env_w + 3) * sizeof(uint2);
+    if (bytes > c->envp_cap) {
+        HIP_TRY(c, hipStreamSynchronize(stream));
+        (void)hipFree(c->d_envp);
+        c->d_envp = nullptr;
+        c->envp_cap = 0;
+        HIP_TRY(c, hipMalloc((void**)&c->d_envp, bytes));
+        c->envp_cap = bytes;
+    }
+    HIP_TRY(c, trt::launch_envp(c->d_env, c->d_envp, c->env_w, c->env_h, stream));
+    c->envp_ok = true;
+    return TRT_OK;
+}
+
 int check_params(trt_ctx* c, const trt_params* p) {
     if (!p) return fail(c, TRT_ERR_INVALID, "trt_render: null params");
     if (!c->have_scene) return fail(c, TRT_ERR_NOSCENE, "trt_render: no scene uploaded");
@@ -531,6 +554,7 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.shade = c->d_shade;
     A.mats = c->d_mats;
     A.env = c->d_env;
+    A.envp = c->envp_ok ? c->d_envp : nullptr;
     A.env_w = c->env_w;
     A.env_h = c->env_h;
     A.counters = c->d_counters;
@@ -750,6 +774,7 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
             c->fev.push_back(e);
         }
     }
+    if ((rc = ensure_envp(c, p, c->stream)) != TRT_OK) return rc;
     KArgs A;
     fill_args(c, p, A);
     A.rays_in = reinterpret_cast<const float*>(p->rays_in);
@@ -825,6 +850,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     const uint32_t rows = trt_output_rows(p);
     const size_t npx = (size_t)rows * p->width;
 
+    if ((rc = ensure_envp(c, p, c->stream)) != TRT_OK) return rc;
     KArgs A;
     fill_args(c, p, A);
 
@@ -954,6 +980,7 @@ extern "C" int trt_upload_envmap_jpeg(trt_ctx* c, const uint8_t* data, size_t le
     }
     (void)hipFree(c->d_env);
     c->d_env = d;
+    c->envp_ok = false;
     c->env_w = (uint32_t)im->width;
     c->env_h = (uint32_t)im->height;
     c->scene_bytes[trt::kSceneEnv] = (size_t)im->width * im->height * 4;
@@ -1056,6 +1083,7 @@ extern "C" int trt_diag_shadow_batch(trt_ctx* c, const trt_params* p, const void
     int rc = check_params(c, p);
     if (rc != TRT_OK) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
+    if ((rc = ensure_envp(c, p, c->stream)) != TRT_OK) return rc;
     KArgs A;
     fill_args(c, p, A);
     HIP_TRY(c, trt::launch_shadow_batch(A, static_cast<const float4*>(rays), n, static_cast<uint32_t*>(occ), c->stream));
