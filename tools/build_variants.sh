@@ -41,6 +41,9 @@ for v in "$@"; do
         prio3) variant prio3 -DTRT_PRIO=3 ;;
         w5) variant w5 -DTRT_WAVES=5 ;;
         tpw2) variant tpw2 -DTRT_TPW=2 ;;
+        persist1) variant persist1 -DTRT_PERSIST=1 -DTRT_PERSIST_WPC=20 ;;
+        persist2) variant persist2 -DTRT_PERSIST=2 -DTRT_PERSIST_WPC=20 ;;
+        persist4) variant persist4 -DTRT_PERSIST=4 -DTRT_PERSIST_WPC=20 ;;
         fmexec) variant fmexec -DTRT_FM_EXEC_BRANCH ;;
         nolds) variant nolds -DTRT_BVH_LDS=0 ;;
         bvh2) variant bvh2 -DTRT_BVH_WIDTH=2 ;;

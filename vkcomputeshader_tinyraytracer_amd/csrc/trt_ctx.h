@@ -46,6 +46,9 @@ struct trt_ctx {
     void* d_rays = nullptr;
     size_t caprays = 0;
     unsigned long long* d_counters = nullptr;
+    // per in-flight slot: per-XCD tile counters of the persistent-grid experiment (TRT_PERSIST
+    // builds, trt_kernel.hip); the last wave of a frame resets them
+    uint32_t* d_persist = nullptr;
     uint32_t num_cus = 256;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
@@ -90,6 +93,8 @@ struct trt_ctx {
     size_t scene_bytes[10] = {0};
     void* diag = nullptr; // diagnostic builds: ray-dump buffer (trt_diag_set_buffer)
 };
+
+constexpr size_t kPersistWords = 8 * 32; // 8 XCDs x (ticket, done) on their own 128-B lines
 
 namespace trt {
 

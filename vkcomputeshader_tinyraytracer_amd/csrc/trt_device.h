@@ -207,6 +207,7 @@ struct KArgs {
     unsigned long long* __restrict__ acc; // per output pixel: fixed-point colour (r, g, b, -)
     uint32_t* __restrict__ spilled;   // output pixels finished by finalize_spilled
     float4* __restrict__ diag;        // diagnostic builds only (TRT_DIAG_DUMP_SHADOW): ray dump
+    uint32_t* __restrict__ persist;   // TRT_PERSIST builds: per-XCD tile tickets of this slot
     // deferred shadows (defer != 0): event log, shadow query queue, per-pixel log heads
     uint32_t defer;
     uint32_t ev_cap;                  // event chunks per stripe (stripe s: chunks [s * ev_cap, ...))

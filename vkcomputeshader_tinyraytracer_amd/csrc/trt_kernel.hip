@@ -1626,7 +1626,32 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
     // 100 MHz constant clock, written to out32 (tools/waveclock.py)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifdef TRT_TPW
+#if defined(TRT_PERSIST)
+    // experiment: persistent waves (grid = a whole GPU's worth); a wave of XCD x = block % 8
+    // takes TRT_PERSIST tiles at a time from its XCD's ticket counter, in xcd_tile order (its
+    // tiles are xcd_tile(j * 8 + x)); the last wave of the XCD to finish resets the counters
+    // for the slot's next frame.  Every wave leaves once the tickets pass the XCD's tiles.
+    {
+        const uint32_t xc = blockIdx.x % 8u;
+        const uint32_t per = A.ntiles > xc ? (A.ntiles - xc + 7u) / 8u : 0u;
+        uint32_t* t = A.persist + xc * 32u;
+        for (;;) {
+            uint32_t j0 = 0;
+            if (lane_id() == 0) j0 = atomicAdd(t, (uint32_t)TRT_PERSIST);
+            j0 = __shfl(j0, 0, 64);
+            if (j0 >= per) break;
+            const uint32_t j1 = min(j0 + (uint32_t)TRT_PERSIST, per);
+            for (uint32_t j = j0; j < j1; ++j) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, xcd_tile(A, j * 8u + xc), cnt, lds, slab);
+        }
+        if (lane_id() == 0) {
+            const uint32_t nw = (gridDim.x - xc + 7u) / 8u;
+            if (atomicAdd(t + 16, 1u) == nw - 1u) {
+                atomicExch(t, 0u);
+                atomicExch(t + 16, 0u);
+            }
+        }
+    }
+#elif defined(TRT_TPW)
     // diagnostic: TRT_TPW tiles per wave, grid-strided (b, b + G, ...; G % 8 == 0 keeps XCDs)
     for (uint32_t k = 0; k < TRT_TPW; ++k) {
         const uint32_t b = blockIdx.x + k * gridDim.x;
@@ -1929,7 +1954,10 @@ hipError_t launch_shadow_batch(const KArgs& A0, const float4* rays, uint32_t n, 
 // depth windows: the tile kernel, one trace_tasks round per further window, finalize_spilled.
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const uint32_t D = A.max_depth;
-#ifdef TRT_TPW
+#if defined(TRT_PERSIST)
+    // experiment: one GPU's worth of waves (TRT_PERSIST_WPC waves per CU)
+    const dim3 grid(A.num_cus * TRT_PERSIST_WPC), block(64);
+#elif defined(TRT_TPW)
     const dim3 grid((A.ntiles + TRT_TPW - 1) / TRT_TPW), block(64);
 #elif TRT_WPB > 1
     const dim3 grid(((A.ntiles + 8 * TRT_WPB - 1) / (8 * TRT_WPB)) * 8), block(64 * TRT_WPB);

@@ -177,7 +177,9 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipSetDevice(hip_device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 32 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 32 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&c->d_persist, kPersistWords * TRT_MAX_FRAMES_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(c->d_persist, 0, kPersistWords * TRT_MAX_FRAMES_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess) {
         trt_destroy(c);
         return TRT_ERR_HIP;
     }
@@ -201,6 +203,7 @@ int trt_destroy(trt_ctx* c) {
     (void)hipFree(c->d_out32);
     (void)hipFree(c->d_rays);
     (void)hipFree(c->d_counters);
+    (void)hipFree(c->d_persist);
     for (hipEvent_t e : c->fev) (void)hipEventDestroy(e);
     for (auto& b : c->split) {
         (void)hipFree(b.q[0]);
@@ -672,6 +675,7 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     A.split_w = 0;
     A.split_d1 = A.max_depth;
     A.num_cus = c->num_cus;
+    A.persist = c->d_persist + (size_t)slot * kPersistWords;
     A.defer = 0;
     const bool defer = defer_frame(c, p);
     // A COUNT frame of a scene whose frames run deferred is traced unsplit, so its image is the
