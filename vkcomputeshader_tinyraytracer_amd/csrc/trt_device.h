@@ -112,7 +112,7 @@ struct alignas(16) Task {
 };
 static_assert(sizeof(Task) == 32, "Task is 32 B");
 constexpr uint32_t kTaskDepthBits = 5u;
-constexpr uint32_t kMaxSplitRounds = 16u;
+constexpr uint32_t kMaxSplitRounds = 20u; // a window of 1 at max_depth 20 (deferred frames)
 // Device counters of one frame's split launches (one set per frames-in-flight slot).
 struct SplitCtr {
     uint32_t spilled;                  // pixels finished by finalize_spilled
@@ -133,7 +133,7 @@ constexpr uint32_t kEvConst = 0xFFFFFFFFu; // plane0.w of an event whose colour 
 // plane0.w of a LINK event (deferred frames with a subtree split): "here come the events of a
 // subtree traced by another lane", plane0 = (first chunk, events, lane, kEvLink) of its chain.
 constexpr uint32_t kEvLink = 0xFFFFFFFEu;
-constexpr uint32_t kMaxLinkDepth = 10u; // nested subtree chains: max_depth / window <= 20 / 2
+constexpr uint32_t kMaxLinkDepth = 20u; // nested subtree chains: max_depth / window <= 20
 // The event pool and the query queue are split into kDeferStripes stripes (tile t allocates
 // from stripe hash(t), each with its own counter on its own 64-B line): one counter
 // for a whole 4K frame serialises ~10^6 wave-aggregated atomics in one L2 channel (measured:

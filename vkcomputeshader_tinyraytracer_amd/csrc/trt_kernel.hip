@@ -1676,8 +1676,8 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
     if (COUNT) flush_counts(A, cnt);
 }
 
-// One round of a split frame: persistent waves pull 64 tasks at a time (one atomic per wave)
-// from the previous launch's queue, trace each task's subtree within the depth window (its
+// One round of a split frame: persistent waves take 64 tasks at a time (static schedule) from
+// the previous launch's queue, trace each task's subtree within the depth window (its
 // window-edge children go to the next queue) and add the subtree's colour to its pixel's
 // fixed-point sum.  Every wave leaves once the queue is drained.
 //
@@ -1690,11 +1690,9 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = min(*A.q_in_n, A.q_cap);
-    for (;;) {
-        uint32_t base = 0;
-        if (threadIdx.x == 0) base = atomicAdd(A.q_in_head, 64u);
-        base = __shfl(base, 0, 64);
-        if (base >= n) break;
+    // static schedule: wave b takes the 64-task blocks b, b + G, ... (a dequeue atomic per block
+    // on one device-scope counter cost ~4x the tasks' own work: profiles/r02_ab_tasks_static.log)
+    for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
         const uint32_t t = base + threadIdx.x;
         if (t < n) {
             const float4* q = reinterpret_cast<const float4*>(A.q_in + t);
@@ -1882,7 +1880,7 @@ static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
     KArgs A = A0;
     const uint32_t stages = defer_stages();
     const uint32_t D = A.max_depth, W = A.split_w;
-    if (HYB && W >= 2 && W < D && A.ctr && A.q_link_buf[0]) {
+    if (HYB && W >= 1 && W < D && A.ctr && A.q_link_buf[0]) {
         // subtree split: the tile kernel traces depths < W, each round the next window
         A.split_d1 = W;
         A.q_out = A.q_buf[0];
@@ -1967,7 +1965,7 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
     if (A.defer && !count && A.spp <= 1 && A.dctr && A.ev && A.shq && A.px_ev && A.fb) {
         hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
-        if (e == hipSuccess && A.split_w >= 2 && A.ctr) e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
+        if (e == hipSuccess && A.split_w >= 1 && A.ctr) e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
         if (e != hipSuccess) return e;
 #define TRT_DEFER_G(CAP, HYB)                                                \
     do {                                                                     \

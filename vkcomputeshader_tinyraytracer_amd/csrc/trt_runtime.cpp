@@ -595,6 +595,9 @@ uint32_t split_window(const trt_ctx* c, const trt_params* p) {
     if ((p->spp > 1) || c->subtree_split == TRT_SPLIT_OFF) return 0;
     if ((size_t)trt_output_rows(p) * p->width >= (1u << (32 - trt::kTaskDepthBits))) return 0;
     uint32_t w;
+    // experiment: a deferred frame traced one depth per launch (TRT_DEFER_WAVEFRONT=1)
+    if (const char* e = std::getenv("TRT_DEFER_WAVEFRONT"))
+        if (std::atoi(e) != 0 && defer_frame(c, p) && D > 1) return 1u;
     if (c->subtree_split == TRT_SPLIT_AUTO) {
         // measured (profiles/r01_split_sweep.log): -10..-16 % on the shipped depth-20 frame with
         // w = 4; +0..+25 % on depth-4 mesh frames (C3/C4) for any window, so only deep trees.
