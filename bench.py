@@ -33,6 +33,10 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
+# frames in flight are HIP streams: 16 hardware queues (HIP's default, 4, is what the box's
+# environment sets) before any HIP init in this process
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector, FMA = 2 flops (AMD spec)
@@ -49,8 +53,9 @@ def parse():
     ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5", "ref", "readme"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="frames in flight (trt_set_frames_in_flight; the reference's MAX_FRAMES_IN_FLIGHT = 2)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight (trt_set_frames_in_flight: 0 = auto = 4, or 8 for deferred-shadow "
+                         "frames; the reference's MAX_FRAMES_IN_FLIGHT is 2)")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (trt_set_subtree_split: 0 auto, 1 off)")
     ap.add_argument("--band-rows", type=int, default=8, help="rows per band of the tiled frames")
     ap.add_argument("--frames-per-gather", type=int, default=8,
@@ -221,7 +226,7 @@ def frame_loop(dev: int, scene, frames: int, warmup: int, inflight: int, split: 
         out8 = torch.empty((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
         stream = torch.cuda.Stream()
         r.set_stream(stream)
-        r.set_frames_in_flight(max(1, inflight))
+        r.set_frames_in_flight(inflight)
         r.render_frames(p, out8, warmup)
         box = {}
         elapsed = timed(g or Group(1, 0), lambda: box.update(n=r.render_frames(p, out8, frames, timing=True,
@@ -230,6 +235,14 @@ def frame_loop(dev: int, scene, frames: int, warmup: int, inflight: int, split: 
         return elapsed, kern_ms, st, p
     finally:
         r.close()
+
+
+def resolved_inflight(inflight: int, scene) -> int:
+    """The library's frames in flight for this scene: the explicit count, or its auto rule (8
+    for deferred-shadow frames: meshes at max_depth >= 8 and spp 1, else 4)."""
+    if inflight:
+        return inflight
+    return 8 if (len(scene.models) > 0 and scene.max_depth >= 8 and scene.spp <= 1) else 4
 
 
 def extra_frame(dev: int, name: str, frames: int, args) -> dict:
@@ -242,7 +255,7 @@ def extra_frame(dev: int, name: str, frames: int, args) -> dict:
     out = {
         "workload": f"{name}: {WORKLOADS[name]}",
         "frames": frames,
-        "frames_in_flight": args.inflight,
+        "frames_in_flight": resolved_inflight(args.inflight, sc),
         "ms_per_frame": round(ms, 4),
         "fps": round(1e3 / ms, 2),
         "mray_s": round(rays / (ms * 1e-3) / 1e6, 3),
@@ -408,7 +421,7 @@ def main():
                 "shadow_rays_per_frame": st["shadow_rays"],
                 "shadow_rays_traced_per_frame": st["shadow_rays"] - st["shadow_skipped"],
                 "parallelism": parallelism,
-                "frames_in_flight": args.inflight,
+                "frames_in_flight": resolved_inflight(args.inflight, scene),
             },
             "roofline": {
                 "bound": "valu",
@@ -420,9 +433,12 @@ def main():
                 "kernel": "trace_kernel",
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 "flops_per_launch": flops,
+                "achieved_per_frame": round(flops / (elapsed1 / K) / 1e12, 3),
+                "frac_per_frame": round(flops / (elapsed1 / K) / 1e12 / VALU_PEAK_TFLOPS, 4),
                 "note": "FP32 flops of the executed work in SURVEY §8d units (counting pass of this frame) / "
                         "the trace kernel's launch time (HIP events on its stream, every 16th launch of the "
-                        "timed loop; with 2 frames in flight a launch's span includes the overlapping frame); "
+                        "timed loop; with several frames in flight a launch's span includes the overlapping "
+                        "frames, so *_per_frame divides by the wall time per frame instead); "
                         "peak counts an FMA as 2 flops, the kernel has no FMA contraction (-ffp-contract=off). "
                         "traffic: no PMC pass in this run (profiles/ holds the PMC summaries of this build)",
                 "hbm_index": {

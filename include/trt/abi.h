@@ -145,9 +145,14 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * no barrier between consecutive compute submissions).  Frame i of a trt_render_frames call
  * runs on in-flight slot i % n: slot 0 is the context's stream, slots 1..n-1 are streams the
  * context owns, forked from and joined back into its stream inside the call, so frame i+1's
- * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 4]; default 2. */
-#define TRT_FRAMES_IN_FLIGHT_DEFAULT 2u
-#define TRT_MAX_FRAMES_IN_FLIGHT 4u
+ * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 8], or 0 = auto
+ * (the default): 4, or 8 for deferred-shadow frames, whose depth-20 trees leave the longest
+ * tails (measured: profiles/r02_ab_queues_*.log).  Each slot is a HIP stream, so the process
+ * needs as many hardware queues: trt_create sets GPU_MAX_HW_QUEUES=16 in the environment when
+ * it is unset and HIP is not yet initialised (HIP's default is 4). */
+#define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
+#define TRT_FRAMES_IN_FLIGHT_AUTO 0u
+#define TRT_MAX_FRAMES_IN_FLIGHT 8u
 int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
 
 /* Subtree split (load balance of deep refraction trees).  The reference traces a pixel's whole

@@ -145,7 +145,7 @@ def test_deferred_frames_in_flight(gpu_renderer, scenes):
     out = torch.empty((6, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
     gpu_renderer.set_deferred_shadows(DEFER_ON)
     try:
-        for n in (1, 2, 3, 4):
+        for n in (1, 2, 3, 4, 8, 0):
             out.zero_()
             gpu_renderer.set_frames_in_flight(n)
             gpu_renderer.render_frames(p, out, 6, frame_stride=p.height * p.width * 4)
@@ -153,7 +153,7 @@ def test_deferred_frames_in_flight(gpu_renderer, scenes):
             for f in range(6):
                 assert np.array_equal(out[f].cpu().numpy(), u8), (n, f)
     finally:
-        gpu_renderer.set_frames_in_flight(2)
+        gpu_renderer.set_frames_in_flight(0)
         gpu_renderer.set_deferred_shadows(DEFER_AUTO)
 
 

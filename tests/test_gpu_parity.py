@@ -250,7 +250,7 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
         assert np.array_equal(out[i].cpu().numpy(), one)
 
 
-@pytest.mark.parametrize("inflight", [1, 2, 3, 4])
+@pytest.mark.parametrize("inflight", [1, 2, 3, 4, 8, 0])
 def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
     """Frames in flight (trt_set_frames_in_flight, main.cpp:45): concurrent frames with
     distinct UBOs and images equal one-at-a-time trt_render, and all of them have landed on
@@ -271,7 +271,7 @@ def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
             snap = out.clone()
         stream.synchronize()
     finally:
-        gpu_renderer.set_frames_in_flight(2)
+        gpu_renderer.set_frames_in_flight(0)
         gpu_renderer.set_stream(None)
     for i in range(n):
         gpu_renderer.update_ubo(ubos[i])
@@ -280,10 +280,10 @@ def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
 
 
 def test_frames_in_flight_bounds(gpu_renderer):
-    for bad in (0, 5):
+    for bad in (9, 100):
         with pytest.raises(TrtError):
             gpu_renderer.set_frames_in_flight(bad)
-    gpu_renderer.set_frames_in_flight(2)
+    gpu_renderer.set_frames_in_flight(0)
 
 
 def test_duplicate_triangles_first_batch_wins(gpu_renderer):

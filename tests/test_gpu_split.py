@@ -114,7 +114,7 @@ def test_split_with_frames_in_flight(gpu_renderer, scenes, defer):
             one, _, _ = gpu_renderer.draw_frame(sc.params())
             assert np.array_equal(out[i].cpu().numpy(), one), i
     finally:
-        gpu_renderer.set_frames_in_flight(2)
+        gpu_renderer.set_frames_in_flight(0)
         gpu_renderer.set_subtree_split(0)
         gpu_renderer.set_deferred_shadows(0)
         gpu_renderer.set_stream(None)

@@ -13,6 +13,8 @@ import sys
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:  # as the library (frames in flight = streams)
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 
 def main():
@@ -23,7 +25,7 @@ def main():
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--depth", type=int, default=0)
     ap.add_argument("--tag", default="")
-    ap.add_argument("--inflight", type=int, default=2, help="frames in flight")
+    ap.add_argument("--inflight", type=int, default=0, help="frames in flight (0 = the library's auto)")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (0 auto, 1 off, 2..5)")
     ap.add_argument("--defer", type=int, default=0, help="deferred shadows (0 auto, 1 off, 2 on)")
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=None, help="override trt_params.flags")

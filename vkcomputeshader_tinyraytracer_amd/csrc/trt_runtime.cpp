@@ -167,6 +167,12 @@ int trt_create(trt_ctx** out, int hip_device) {
     *out = nullptr;
     trt_ctx* c = new (std::nothrow) trt_ctx();
     if (!c) return TRT_ERR_OOM;
+    // frames in flight are HIP streams: ask for 16 hardware queues when the environment leaves
+    // HIP at its default of 4 (or less); no effect once HIP is initialised in this process
+    {
+        const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+        if (!q || std::atoi(q) <= 4) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+    }
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0 || hip_device < 0 || hip_device >= n) {
@@ -244,8 +250,8 @@ int trt_set_stream(trt_ctx* c, void* s) {
 
 int trt_set_frames_in_flight(trt_ctx* c, uint32_t n) {
     if (!c) return TRT_ERR_INVALID;
-    if (n < 1 || n > TRT_MAX_FRAMES_IN_FLIGHT)
-        return fail(c, TRT_ERR_INVALID, "trt_set_frames_in_flight: n must be in [1, TRT_MAX_FRAMES_IN_FLIGHT]");
+    if (n > TRT_MAX_FRAMES_IN_FLIGHT)
+        return fail(c, TRT_ERR_INVALID, "trt_set_frames_in_flight: n must be 0 (auto) or in [1, TRT_MAX_FRAMES_IN_FLIGHT]");
     c->frames_in_flight = n;
     return TRT_OK;
 }
@@ -789,7 +795,10 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
     // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): frame i runs on slot i % n.  Slot 0
     // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
     // joined back into it below, so to the caller all frames complete on its stream.
-    const uint32_t nfl = std::min(c->frames_in_flight, std::max(nframes, 1u));
+    // auto: 4, or 8 for deferred-shadow frames (C2 -13 % at 4 vs 2; the shipped frame 1.45 ->
+    // 0.56 ms at 8: profiles/r02_ab_queues_c2.log, r02_ab_queues_deep.log)
+    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : (defer_frame(c, p) ? 8u : 4u);
+    const uint32_t nfl = std::min(want, std::max(nframes, 1u));
     std::vector<hipStream_t> sv{c->stream};
     if (nfl > 1) {
         while (c->aux.size() < nfl - 1) {
