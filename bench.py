@@ -363,7 +363,16 @@ def main():
     if world == 1:
         value, ms_per_step = weak_value, elapsed1 / K * 1e3
         scaling, parallelism = "weak", "1 GPU"
-        headline_extra = None
+        # the N > 1 headline's path (trt_render_multi_frames) at one rank: the base of its
+        # strong-scaling curve, so the driver's per-N values can be read against it
+        elapsed_t, mst, _, _ = tiled_stream(g, dev, multi, scene, K, args.warmup, args.band_rows, ROOT_ROTATE,
+                                            args.frames_per_gather)
+        rays_whole = mst["primary_rays"] + mst["secondary_rays"]
+        headline_extra = {"tiled_headline_1gpu": {
+            "value": round(rays_whole * K / elapsed_t / 1e6, 3), "unit": "Mray/s",
+            "ms_per_step": round(elapsed_t / K * 1e3, 5),
+            "workload": f"the N > 1 headline's path at 1 rank: {args.config} through trt_render_multi_frames "
+                        f"({args.band_rows}-row bands, RCCL gather of {args.frames_per_gather} frames per op)"}}
     else:
         # the frame row-tiled over all GPUs, RCCL gathers of --frames-per-gather frames on a rotating root
         elapsed, mst, _, _ = tiled_stream(g, dev, multi, scene, K, args.warmup, args.band_rows, ROOT_ROTATE,

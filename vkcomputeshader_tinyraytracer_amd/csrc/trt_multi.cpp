@@ -196,20 +196,24 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         if (d.gathered_valid[slot]) MHIP(m, hipStreamWaitEvent(rs, d.gathered[slot], 0));
         hipStream_t keep = d.ctx->stream;
         d.ctx->stream = rs;
-        for (uint32_t f = 0; f < nf; ++f) {
-            if (ubos) d.ctx->ubo = ubos[f];
-            for (uint32_t v = 0; v < G; ++v) {
-                const uint32_t g = d.rank * G + v;
-                if (!rows[g]) continue;
-                trt_params q = group_params(p, band_rows, NG, g);
-                q.flags &= ~(TRT_FLAG_COUNT | TRT_FLAG_TIMING);
-                const int rc = trt_render(d.ctx, &q, d.local[slot] + (f * G + v) * blk, nullptr, nullptr);
-                if (rc != TRT_OK) {
-                    d.ctx->stream = keep;
-                    return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
-                }
+        // the batch's frames of each band group through the context's frame loop, so they run
+        // with its frames in flight (frame f's group v lands at local + (f * G + v) * blk)
+        for (uint32_t v = 0; v < G; ++v) {
+            const uint32_t g = d.rank * G + v;
+            if (!rows[g]) continue;
+            trt_params q = group_params(p, band_rows, NG, g);
+            q.flags &= ~(TRT_FLAG_COUNT | TRT_FLAG_TIMING);
+            q.flags |= TRT_FLAG_DEVICE_PTRS;
+            // the root's own groups go straight to their place in the gather buffer (no send)
+            const bool own = d.rank == root;
+            uint8_t* dst = own ? d.gather[slot] + (size_t)g * blk : d.local[slot] + v * blk;
+            const int rc = trt_render_frames(d.ctx, &q, ubos, nf, dst, (own ? NG : G) * blk, 0);
+            if (rc != TRT_OK) {
+                d.ctx->stream = keep;
+                return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
             }
         }
+        if (ubos) d.ctx->ubo = ubos[nf - 1];
         d.ctx->stream = keep;
         MHIP(m, hipEventRecord(d.rendered[slot], rs));
         MHIP(m, hipStreamWaitEvent(d.comm_stream, d.rendered[slot], 0));
@@ -219,15 +223,17 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
     for (auto& d : m->devs) {
         MHIP(m, hipSetDevice(d.device));
         for (uint32_t f = 0; f < nf; ++f) {
-            for (uint32_t v = 0; v < G; ++v) {
-                const uint32_t g = d.rank * G + v;
-                if (rows[g])
-                    MNCCL(m, ncclSend(d.local[slot] + (f * G + v) * blk, (size_t)rows[g] * W * 4, ncclUint8, (int)root,
-                                      d.comm, d.comm_stream));
+            if (d.rank != root) {
+                for (uint32_t v = 0; v < G; ++v) {
+                    const uint32_t g = d.rank * G + v;
+                    if (rows[g])
+                        MNCCL(m, ncclSend(d.local[slot] + (f * G + v) * blk, (size_t)rows[g] * W * 4, ncclUint8,
+                                          (int)root, d.comm, d.comm_stream));
+                }
+                continue;
             }
-            if (d.rank != root) continue;
             for (uint32_t g = 0; g < NG; ++g)
-                if (rows[g])
+                if (rows[g] && g / G != root)
                     MNCCL(m, ncclRecv(d.gather[slot] + (f * NG + g) * blk, (size_t)rows[g] * W * 4, ncclUint8,
                                       (int)(g / G), d.comm, d.comm_stream));
         }
