@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""trt_render_multi_frames on this process's GPUs (default: device 0 only) for one config:
+wall time per frame, and with a rocprofv3 kernel trace (tools/multi_probe.sh) the GPU busy
+fraction of the timed loop.
+
+  python tools/multi_probe.py --config C2 --frames 400 --per-gather 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--frames", type=int, default=400)
+    ap.add_argument("--per-gather", type=int, default=8)
+    ap.add_argument("--band-rows", type=int, default=8)
+    a = ap.parse_args()
+    import torch
+
+    from vkcomputeshader_tinyraytracer_amd import scene as S
+    from vkcomputeshader_tinyraytracer_amd.multi import ROOT_ROTATE, MultiRenderer
+
+    sc = S.CONFIGS[a.config]()
+    p = sc.params()
+    m = MultiRenderer(devices=(0,))
+    m.upload_scene(sc)
+    out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    m.render_frames(p, 16, a.band_rows, ROOT_ROTATE, a.per_gather, outs=[out])
+    m.synchronize()
+    t0 = time.perf_counter()
+    m.render_frames(p, a.frames, a.band_rows, ROOT_ROTATE, a.per_gather, outs=[out])
+    t1 = time.perf_counter()
+    m.synchronize()
+    t2 = time.perf_counter()
+    print(json.dumps({"config": a.config, "frames": a.frames, "per_gather": a.per_gather,
+                      "host_enqueue_us_per_frame": round((t1 - t0) / a.frames * 1e6, 2),
+                      "wall_us_per_frame": round((t2 - t0) / a.frames * 1e6, 2)}), flush=True)
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
