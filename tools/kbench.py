@@ -65,11 +65,16 @@ def main():
     torch.cuda.synchronize()
     # wall per frame of a back-to-back batch without per-frame events (one event pair)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    import time
+    torch.cuda.synchronize()
     e0.record(stream)
+    t0 = time.perf_counter()
     r.render_frames(p, out, a.frames)
+    t1 = time.perf_counter()
     e1.record(stream)
     torch.cuda.synchronize()
     wall_noev = e0.elapsed_time(e1) / a.frames
+    host_us = (t1 - t0) / a.frames * 1e6
     e0.record(stream)
     r.render_frames(p, out, a.frames, timing=True, time_every=16)
     e1.record(stream)
@@ -80,7 +85,7 @@ def main():
            "size": [p.width, p.height], "depth": p.max_depth, "rays": rays,
            "med_us": round(float(np.median(ms)) * 1e3, 2), "min_us": round(float(ms.min()) * 1e3, 2),
            "Mray_s_kernel": round(rays / (float(np.median(ms)) * 1e-3) / 1e6, 1),
-           "wall_us_no_events": round(wall_noev * 1e3, 2), "wall_us_events_every16": round(wall_ev * 1e3, 2)}
+           "wall_us_no_events": round(wall_noev * 1e3, 2), "host_enqueue_us": round(host_us, 2), "wall_us_events_every16": round(wall_ev * 1e3, 2)}
     if a.defer != 1:
         res["defer_stats"] = r.defer_stats(0)
     print(json.dumps(res), flush=True)
