@@ -62,6 +62,10 @@ extern "C" {
                                           (the B8G8R8A8_SRGB swapchain, main.cpp:2341, that
                                           shader.frag writes the sampled image to); out_rgba32f
                                           stays rayOut */
+#define TRT_FLAG_BAND_IN_PLACE (1u << 10) /* with band params: each rendered row is written at its
+                                          row of a full width*height image instead of compactly
+                                          (several bands render into one frame); needs
+                                          TRT_FLAG_DEVICE_PTRS */
 
 /* The shipped shader: floor on, spheres off, envmap background, host ray quirk. */
 #define TRT_FLAGS_REFERENCE (TRT_FLAG_FLOOR | TRT_FLAG_ENVMAP | TRT_FLAG_ROW_QUIRK)

@@ -140,6 +140,31 @@ def test_bands_equal_rows_of_full_frame(gpu_renderer):
         assert sorted(sum(parts, [])) == list(range(sc.height))
 
 
+@pytest.mark.parametrize("which", ["C2", "reference"])
+def test_bands_in_place_assemble_the_frame(gpu_renderer, golden_meshes, which):
+    """TRT_FLAG_BAND_IN_PLACE: each band launch writes its rows at their frame rows, so the
+    bands of one frame rendered into one device image give the whole frame (the multi-GPU root
+    renders its own bands this way); also through the deferred-shadow passes."""
+    torch = pytest.importorskip("torch")
+    sc = (S.config_c2(128, 100, env_size=SMALL_ENV) if which == "C2" else
+          S.config_reference_default(golden_meshes, env_size=SMALL_ENV, width=160, height=120))
+    gpu_renderer.upload_scene(sc)
+    full, full32, _ = gpu_renderer.draw_frame(sc.params(), want32=True)
+    out8 = torch.zeros((sc.height, sc.width, 4), dtype=torch.uint8, device="cuda")
+    out32 = torch.zeros((sc.height, sc.width, 4), dtype=torch.float32, device="cuda")
+    for idx in range(3):
+        p = sc.params(band_rows=8, band_count=3, band_index=idx)
+        p.flags |= T.FLAG_BAND_IN_PLACE
+        gpu_renderer.draw_frame(p, out8=out8, out32=out32)
+    torch.cuda.synchronize()
+    assert np.array_equal(out8.cpu().numpy(), full)
+    assert np.array_equal(out32.cpu().numpy(), full32)
+    p = sc.params(band_rows=8, band_count=3, band_index=0)
+    p.flags |= T.FLAG_BAND_IN_PLACE
+    with pytest.raises(TrtError):  # host outputs cannot hold a band in place
+        gpu_renderer.draw_frame(p)
+
+
 def test_rays_in_replay(gpu_renderer):
     """Binding 1 replay: host rays built as main.cpp:1496-1506 does give the same frame."""
     sc = S.config_c2(96, 64, env_size=SMALL_ENV)

@@ -1447,6 +1447,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 // Gamma (shader.comp:598) and the dual store (rayOut binding 2, storage image binding 3) of
 // output pixel o; `c` is the clamped colour.
 __device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
+    if (A.flags & TRT_FLAG_BAND_IN_PLACE) { // compact row k -> its frame row (band_row)
+        const uint32_t k = (uint32_t)(o / A.width), x = (uint32_t)(o % A.width);
+        o = (size_t)band_row(A, k) * A.width + x;
+    }
     const float gx = pow_pos(c.x, TRT_GAMMA), gy = pow_pos(c.y, TRT_GAMMA), gz = pow_pos(c.z, TRT_GAMMA);
 #ifdef TRT_DIAG_WAVE_CLOCK
     if (false) // out32 carries the workgroup clock records
@@ -2065,9 +2069,11 @@ namespace trt {
 
 __global__ __launch_bounds__(256) void interleave_kernel(const uint32_t* __restrict__ gather, uint32_t* __restrict__ out,
                                                          uint32_t W, uint32_t H, uint32_t B, uint32_t NG,
-                                                         uint32_t max_rows, size_t stride_px, int vec4) {
+                                                         uint32_t max_rows, size_t stride_px, int vec4,
+                                                         uint32_t skip_lo, uint32_t skip_hi) {
     const uint32_t f = blockIdx.x / H, y = blockIdx.x % H;
     const uint32_t b = y / B, g = b % NG, k = (b / NG) * B + y % B;
+    if (g >= skip_lo && g < skip_hi) return; // the root's own groups, rendered in place
     const uint32_t* src = gather + ((size_t)(f * NG + g) * max_rows + k) * W;
     uint32_t* dst = out + (size_t)f * stride_px + (size_t)y * W;
     if (vec4) {
@@ -2081,12 +2087,13 @@ __global__ __launch_bounds__(256) void interleave_kernel(const uint32_t* __restr
 
 hipError_t launch_interleave(const uint32_t* gather, uint32_t* out, uint32_t width, uint32_t height,
                              uint32_t band_rows, uint32_t groups, uint32_t max_rows, uint32_t nframes,
-                             size_t frame_stride_px, hipStream_t stream) {
+                             size_t frame_stride_px, hipStream_t stream, uint32_t skip_lo, uint32_t skip_hi) {
+    if (skip_lo == 0 && skip_hi >= groups) return hipSuccess; // every group was rendered in place
     if (!width || !height || !nframes) return hipSuccess;
     const int vec4 = (width % 4u == 0u) && ((reinterpret_cast<uintptr_t>(out) & 15u) == 0u) &&
                      (frame_stride_px % 4u == 0u) && ((reinterpret_cast<uintptr_t>(gather) & 15u) == 0u);
     hipLaunchKernelGGL(interleave_kernel, dim3(height * nframes), dim3(256), 0, stream, gather, out, width, height,
-                       band_rows, groups, max_rows, frame_stride_px, vec4);
+                       band_rows, groups, max_rows, frame_stride_px, vec4, skip_lo, skip_hi);
     return hipGetLastError();
 }
 

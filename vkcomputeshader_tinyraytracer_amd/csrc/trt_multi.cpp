@@ -33,7 +33,7 @@
 namespace trt {
 hipError_t launch_interleave(const uint32_t* gather, uint32_t* out, uint32_t width, uint32_t height,
                              uint32_t band_rows, uint32_t groups, uint32_t max_rows, uint32_t nframes,
-                             size_t frame_stride_px, hipStream_t stream);
+                             size_t frame_stride_px, hipStream_t stream, uint32_t skip_lo, uint32_t skip_hi);
 }
 
 struct trt_multi {
@@ -190,7 +190,10 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
             return TRT_ERR_HIP;
     }
     // render
+    size_t di = 0;
     for (auto& d : m->devs) {
+        uint8_t* frame_out = (d.rank == root && out8) ? out8[di] : nullptr;
+        ++di;
         MHIP(m, hipSetDevice(d.device));
         hipStream_t rs = d.render[slot];
         if (d.gathered_valid[slot]) MHIP(m, hipStreamWaitEvent(rs, d.gathered[slot], 0));
@@ -204,10 +207,20 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
             trt_params q = group_params(p, band_rows, NG, g);
             q.flags &= ~(TRT_FLAG_COUNT | TRT_FLAG_TIMING);
             q.flags |= TRT_FLAG_DEVICE_PTRS;
-            // the root's own groups go straight to their place in the gather buffer (no send)
+            // the root's own groups: rendered in place into the output frames when there are
+            // any (no send, no re-interleave), else straight into the gather buffer
             const bool own = d.rank == root;
-            uint8_t* dst = own ? d.gather[slot] + (size_t)g * blk : d.local[slot] + v * blk;
-            const int rc = trt_render_frames(d.ctx, &q, ubos, nf, dst, (own ? NG : G) * blk, 0);
+            uint8_t* dst = d.local[slot] + v * blk;
+            size_t stride = G * blk;
+            if (own && frame_out) {
+                q.flags |= TRT_FLAG_BAND_IN_PLACE;
+                dst = frame_out;
+                stride = frame_stride;
+            } else if (own) {
+                dst = d.gather[slot] + (size_t)g * blk;
+                stride = NG * blk;
+            }
+            const int rc = trt_render_frames(d.ctx, &q, ubos, nf, dst, stride, 0);
             if (rc != TRT_OK) {
                 d.ctx->stream = keep;
                 return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
@@ -245,7 +258,7 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         if (d.rank == root && out8 && out8[li]) {
             MHIP(m, trt::launch_interleave(reinterpret_cast<const uint32_t*>(d.gather[slot]),
                                            reinterpret_cast<uint32_t*>(out8[li]), W, H, band_rows, NG, max_rows, nf,
-                                           frame_stride / 4, d.comm_stream));
+                                           frame_stride / 4, d.comm_stream, root * G, root * G + G));
         }
         MHIP(m, hipEventRecord(d.gathered[slot], d.comm_stream));
         d.gathered_valid[slot] = true;

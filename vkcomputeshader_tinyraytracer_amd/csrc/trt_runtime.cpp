@@ -536,6 +536,8 @@ int check_params(trt_ctx* c, const trt_params* p) {
     if (p->spp > 4096) return fail(c, TRT_ERR_INVALID, "trt_render: spp must be <= 4096");
     if (p->band_rows && p->band_count > 1 && p->band_index >= p->band_count)
         return fail(c, TRT_ERR_INVALID, "trt_render: band_index >= band_count");
+    if ((p->flags & TRT_FLAG_BAND_IN_PLACE) && !(p->flags & TRT_FLAG_DEVICE_PTRS))
+        return fail(c, TRT_ERR_INVALID, "trt_render: TRT_FLAG_BAND_IN_PLACE needs TRT_FLAG_DEVICE_PTRS");
     if ((p->flags & TRT_FLAG_ENVMAP) && !c->d_env)
         return fail(c, TRT_ERR_INVALID, "trt_render: TRT_FLAG_ENVMAP without an uploaded envmap");
     return TRT_OK;

@@ -100,6 +100,8 @@ class Renderer:
         Returns (rgba8, rgba32f, stats_dict)."""
         p = T.Params.from_buffer_copy(params)
         rows = int(self._L.trt_output_rows(ctypes.byref(p)))
+        if p.flags & T.FLAG_BAND_IN_PLACE:  # bands written at their frame rows: full-size outputs
+            rows = p.height
         dev = _is_torch_cuda(out8) or _is_torch_cuda(out32) or _is_torch_cuda(rays_in)
         if dev:
             p.flags |= T.FLAG_DEVICE_PTRS

@@ -59,6 +59,7 @@ FLAG_COUNT = 1 << 6
 FLAG_TIMING = 1 << 7
 FLAG_BATCH_WALK = 1 << 8
 FLAG_SRGB_OUT = 1 << 9
+FLAG_BAND_IN_PLACE = 1 << 10  # band rows written at their frame rows (device outputs)
 FLAGS_REFERENCE = FLAG_FLOOR | FLAG_ENVMAP | FLAG_ROW_QUIRK
 
 MAX_DEPTH_LIMIT = 20
