@@ -41,6 +41,10 @@ for v in "$@"; do
         prio3) variant prio3 -DTRT_PRIO=3 ;;
         w5) variant w5 -DTRT_WAVES=5 ;;
         tpw2) variant tpw2 -DTRT_TPW=2 ;;
+        dlds1) variant dlds1 -DTRT_DEFER_LDS=1 ;;
+        dlds2) variant dlds2 -DTRT_DEFER_LDS=2 ;;
+        dlds4) variant dlds4 -DTRT_DEFER_LDS=4 ;;
+        dlds4b16) variant dlds4b16 -DTRT_DEFER_LDS=4 -DTRT_BVH_LDS_N=16 ;;
         persist1) variant persist1 -DTRT_PERSIST=1 -DTRT_PERSIST_WPC=20 ;;
         persist2) variant persist2 -DTRT_PERSIST=2 -DTRT_PERSIST_WPC=20 ;;
         persist4) variant persist4 -DTRT_PERSIST=4 -DTRT_PERSIST_WPC=20 ;;

@@ -1879,6 +1879,9 @@ static uint32_t defer_stages() { // debug: TRT_DEFER_STAGES bitmask of passes to
     return e ? (uint32_t)strtoul(e, nullptr, 0) : 0xFFu;
 }
 
+#ifndef TRT_DEFER_LDS
+#define TRT_DEFER_LDS 3 /* deferred refraction children of a deep deferred frame kept in LDS */
+#endif
 template <int CAP, int GEOM, bool HYB>
 static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 block) {
     KArgs A = A0;
@@ -1978,12 +1981,12 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
         else if (geom == 2) launch_defer<CAP, 2, HYB>(A, stream, grid, block); \
         else launch_defer<CAP, 3, HYB>(A, stream, grid, block);              \
     } while (0)
-        // deep trees: 3 deferred children in LDS + a private tail (the split launches' LDS budget)
+        // deep trees: TRT_DEFER_LDS deferred children in LDS + a private tail
         if (D <= 1) TRT_DEFER_G(0, false);
         else if (D <= 2) TRT_DEFER_G(1, false);
         else if (D <= 3) TRT_DEFER_G(2, false);
         else if (D <= 4) TRT_DEFER_G(3, false);
-        else TRT_DEFER_G(3, true);
+        else TRT_DEFER_G(TRT_DEFER_LDS, true);
 #undef TRT_DEFER_G
         return hipGetLastError();
     }
