@@ -58,7 +58,7 @@ def parse():
                          "frames; the reference's MAX_FRAMES_IN_FLIGHT is 2)")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (trt_set_subtree_split: 0 auto, 1 off)")
     ap.add_argument("--band-rows", type=int, default=8, help="rows per band of the tiled frames")
-    ap.add_argument("--frames-per-gather", type=int, default=32,
+    ap.add_argument("--frames-per-gather", type=int, default=64,
                     help="frames whose bands move in one RCCL gather (N > 1 headline)")
     ap.add_argument("--tiled-frames", type=int, default=20,
                     help="frames of the tiled 3840x2160 leg (C4 row-tiled + RCCL gather on rank 0); 0 skips it")

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--per-gather", type=int, default=8)
     ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=0, help="frames in flight of each device context")
     a = ap.parse_args()
     import torch
 
@@ -31,6 +32,9 @@ def main():
     sc = S.CONFIGS[a.config]()
     p = sc.params()
     m = MultiRenderer(devices=(0,))
+    if a.inflight:
+        L = m._L
+        L.trt_set_frames_in_flight(L.trt_multi_context(m._h, 0), a.inflight)
     m.upload_scene(sc)
     out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
     m.render_frames(p, 16, a.band_rows, ROOT_ROTATE, a.per_gather, outs=[out])
@@ -40,7 +44,7 @@ def main():
     t1 = time.perf_counter()
     m.synchronize()
     t2 = time.perf_counter()
-    print(json.dumps({"config": a.config, "frames": a.frames, "per_gather": a.per_gather,
+    print(json.dumps({"config": a.config, "frames": a.frames, "per_gather": a.per_gather, "inflight": a.inflight,
                       "host_enqueue_us_per_frame": round((t1 - t0) / a.frames * 1e6, 2),
                       "wall_us_per_frame": round((t2 - t0) / a.frames * 1e6, 2)}), flush=True)
     m.close()

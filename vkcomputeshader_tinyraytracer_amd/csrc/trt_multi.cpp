@@ -199,6 +199,11 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         if (d.gathered_valid[slot]) MHIP(m, hipStreamWaitEvent(rs, d.gathered[slot], 0));
         hipStream_t keep = d.ctx->stream;
         d.ctx->stream = rs;
+        // a band group's frames are 1/N of a frame each: the auto in-flight count of a tiled
+        // batch is 8 (C2 at 1 rank, 64 frames per gather: 24.4 -> 19.6 us per frame against 4,
+        // profiles/r02_multi_probe_inflight.log)
+        const uint32_t keep_fl = d.ctx->frames_in_flight;
+        if (!keep_fl) d.ctx->frames_in_flight = TRT_MAX_FRAMES_IN_FLIGHT;
         // the batch's frames of each band group through the context's frame loop, so they run
         // with its frames in flight (frame f's group v lands at local + (f * G + v) * blk)
         for (uint32_t v = 0; v < G; ++v) {
@@ -223,11 +228,13 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
             const int rc = trt_render_frames(d.ctx, &q, ubos, nf, dst, stride, 0);
             if (rc != TRT_OK) {
                 d.ctx->stream = keep;
+                d.ctx->frames_in_flight = keep_fl;
                 return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
             }
         }
         if (ubos) d.ctx->ubo = ubos[nf - 1];
         d.ctx->stream = keep;
+        d.ctx->frames_in_flight = keep_fl;
         MHIP(m, hipEventRecord(d.rendered[slot], rs));
         MHIP(m, hipStreamWaitEvent(d.comm_stream, d.rendered[slot], 0));
     }
