@@ -285,7 +285,9 @@ def tiled_stream(g: Group, dev: int, multi, scene, frames: int, warmup: int, ban
     out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
-    multi.render_frames(p, warmup, band_rows, root, per_gather, outs=[out])
+    # warmup: at least one batch of the timed batches' size, so the gather buffers are sized
+    # before timing (the timed batches never allocate)
+    multi.render_frames(p, max(warmup, min(frames, per_gather)), band_rows, root, per_gather, outs=[out])
     elapsed = timed(g, lambda: multi.render_frames(p, frames, band_rows, root, per_gather, outs=[out]))
     multi.set_stream(0, None)
     return elapsed, st, out, p

@@ -72,6 +72,29 @@ def test_render_multi_frames_device_batches(gpu_renderer, multi):
         assert np.array_equal(got[i], one), i
 
 
+def test_render_multi_frames_first_batches_after_upload():
+    """Batches straight after an upload with the full-size envmap: the first batch (slot 0)
+    builds the envmap pair rows, and the second batch's render stream (slot 1) forked before
+    that build, so the build must be complete before any other stream samples them."""
+    torch = pytest.importorskip("torch")
+    from vkcomputeshader_tinyraytracer_amd import Renderer
+
+    sc = S.config_c2(320, 200)  # reference envmap size 7616 x 3808
+    p = sc.params()
+    with Renderer(0) as r:
+        r.upload_scene(sc)
+        want, _, _ = r.draw_frame(p)
+    out = torch.zeros((4, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    with MultiRenderer([0]) as m:
+        m.upload_scene(sc)
+        m.render_frames(p, 4, band_rows=8, root=0, frames_per_gather=1, outs=[out],
+                        frame_stride=p.height * p.width * 4)
+        m.synchronize()
+    got = out.cpu().numpy()
+    for i in range(4):
+        assert np.array_equal(got[i], want), i
+
+
 def test_render_multi_deep_mesh_frame_split_active(gpu_renderer, multi, golden_meshes):
     """Depth-20 mesh frame (the subtree split is on): consecutive batches on the two render
     streams share the context's split scratch only through its stream fences."""

@@ -171,7 +171,7 @@ int check_common(trt_multi* m, const trt_params* p, uint32_t band_rows, int root
 // compact buffer (render stream of the slot), the compact buffers go to the batch's root over
 // RCCL (communication stream), and the root re-interleaves them into out + f * stride.
 int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t nf, uint32_t band_rows,
-              uint32_t root, uint8_t* const* out8, size_t frame_stride) {
+              uint32_t root, bool rotate, uint8_t* const* out8, size_t frame_stride) {
     const uint32_t N = m->nranks, G = m->groups, NG = N * G;
     const uint32_t W = p->width, H = p->height;
     uint32_t max_rows = 0;
@@ -184,11 +184,15 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
     const size_t blk = (size_t)max_rows * W * 4; // one compact band-group buffer
     const int slot = (int)(m->batch_seq & 1u);
     ++m->batch_seq;
-    for (auto& d : m->devs) {
-        if (grow(m, d.device, &d.local[slot], &d.local_cap[slot], blk * G * nf) != TRT_OK) return TRT_ERR_HIP;
-        if (d.rank == root && grow(m, d.device, &d.gather[slot], &d.gather_cap[slot], blk * NG * nf) != TRT_OK)
-            return TRT_ERR_HIP;
-    }
+    // both slots grow together, and with a rotating root every device sizes its gather
+    // buffers, so no batch after the first one of a size allocates (grow synchronizes the
+    // device before it frees a buffer an in-flight batch may read)
+    for (auto& d : m->devs)
+        for (int s = 0; s < 2; ++s) {
+            if (grow(m, d.device, &d.local[s], &d.local_cap[s], blk * G * nf) != TRT_OK) return TRT_ERR_HIP;
+            if ((rotate || d.rank == root) && grow(m, d.device, &d.gather[s], &d.gather_cap[s], blk * NG * nf) != TRT_OK)
+                return TRT_ERR_HIP;
+        }
     // render
     size_t di = 0;
     for (auto& d : m->devs) {
@@ -458,7 +462,7 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
         ++li;
     }
     if ((rc = fork_all(m)) != TRT_OK) return rc;
-    if ((rc = run_batch(m, p, nullptr, 1, band_rows, (uint32_t)root, outs.data(), 0)) != TRT_OK) return rc;
+    if ((rc = run_batch(m, p, nullptr, 1, band_rows, (uint32_t)root, false, outs.data(), 0)) != TRT_OK) return rc;
     if ((rc = join_all(m)) != TRT_OK) return rc;
     li = 0;
     for (auto& d : m->devs) {
@@ -550,7 +554,8 @@ int trt_render_multi_frames(trt_multi* m, const trt_params* p, const trt_ubo* ub
         const uint32_t r = root == TRT_ROOT_ROTATE ? (uint32_t)(m->batch_seq % m->nranks) : (uint32_t)root;
         for (size_t li = 0; li < m->devs.size(); ++li)
             outs[li] = (out8 && out8[li]) ? out8[li] + (size_t)i0 * frame_stride : nullptr;
-        if ((rc = run_batch(m, p, ubos ? ubos + i0 : nullptr, nf, band_rows, r, outs.data(), frame_stride)) != TRT_OK)
+        if ((rc = run_batch(m, p, ubos ? ubos + i0 : nullptr, nf, band_rows, r, root == TRT_ROOT_ROTATE, outs.data(),
+                            frame_stride)) != TRT_OK)
             return rc;
     }
     return join_all(m);

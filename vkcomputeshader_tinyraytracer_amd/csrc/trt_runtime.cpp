@@ -522,6 +522,9 @@ int ensure_envp(trt_ctx* c, const trt_params* p, hipStream_t stream) {
         c->envp_cap = bytes;
     }
     HIP_TRY(c, trt::launch_envp(c->d_env, c->d_envp, c->env_w, c->env_h, stream));
+    // once per envmap upload: wait for the build, since later frames may run on streams not
+    // ordered after `stream` (trt_multi's two batch slots fork before the first batch builds)
+    HIP_TRY(c, hipStreamSynchronize(stream));
     c->envp_ok = true;
     return TRT_OK;
 }
