@@ -33,10 +33,10 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
-# frames in flight are HIP streams: 16 hardware queues (HIP's default, 4, is what the box's
+# frames in flight are HIP streams: 32 hardware queues (HIP's default, 4, is what the box's
 # environment sets) before any HIP init in this process
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector, FMA = 2 flops (AMD spec)

@@ -152,7 +152,7 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 8], or 0 = auto
  * (the default): 4, or 8 for deferred-shadow frames, whose depth-20 trees leave the longest
  * tails (measured: profiles/r02_ab_queues_*.log).  Each slot is a HIP stream, so the process
- * needs as many hardware queues: trt_create sets GPU_MAX_HW_QUEUES=16 in the environment when
+ * needs as many hardware queues: trt_create sets GPU_MAX_HW_QUEUES=32 in the environment when
  * it is unset and HIP is not yet initialised (HIP's default is 4). */
 #define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
 #define TRT_FRAMES_IN_FLIGHT_AUTO 0u

@@ -14,7 +14,7 @@ from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:  # as the library (frames in flight = streams)
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 
 def main():

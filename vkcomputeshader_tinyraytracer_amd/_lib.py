@@ -39,10 +39,10 @@ def lib() -> ctypes.CDLL:
     # /opt/rocm's (7.2, same SONAME).  Measured on the box: when libtrt has initialised HIP
     # before torch is imported, torch's device init fails ("No HIP GPUs are available"); with
     # torch imported first both work.  So when torch is importable it is loaded first.
-    # Frames in flight run on their own HIP streams: 16 hardware queues when the environment
+    # Frames in flight run on their own HIP streams: 32 hardware queues when the environment
     # leaves HIP at its default of 4 (or less), set before torch or libtrt initialises HIP.
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+        os.environ["GPU_MAX_HW_QUEUES"] = "32"
     try:
         import torch  # noqa: F401
     except ImportError:

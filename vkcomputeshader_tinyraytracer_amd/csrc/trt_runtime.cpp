@@ -167,11 +167,11 @@ int trt_create(trt_ctx** out, int hip_device) {
     *out = nullptr;
     trt_ctx* c = new (std::nothrow) trt_ctx();
     if (!c) return TRT_ERR_OOM;
-    // frames in flight are HIP streams: ask for 16 hardware queues when the environment leaves
+    // frames in flight are HIP streams: ask for 32 hardware queues when the environment leaves
     // HIP at its default of 4 (or less); no effect once HIP is initialised in this process
     {
         const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-        if (!q || std::atoi(q) <= 4) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+        if (!q || std::atoi(q) <= 4) setenv("GPU_MAX_HW_QUEUES", "32", 1);
     }
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
