@@ -3,22 +3,27 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|ref|readme] [--no-cpu]
 
-One step = one frame of the configuration (C2 by default), inputs resident in HBM.
+Every frame has its own UBO: the camera walks like the reference's interactive loop with W and
+D held (processInput + updateUniformBuffer, main.cpp:391-403, 2165-2179), cycling through
+--camera-period positions whose ray counts come from one counting pass each (excluded from
+timing).  Inputs are resident in HBM; the timed region only enqueues and runs frames.
 
-* N = 1: the frame loop of the C-ABI (trt_render_frames, 2 frames in flight) on one GPU.
-* N > 1 (one process per GPU under torch.distributed.run): every frame is row-tiled over the
-  N GPUs and gathered over RCCL by the native multi-GPU path (trt_render_multi_frames,
-  csrc/trt_multi.cpp): strong scaling, the frame is fixed and each GPU renders 1/N of it.
-  Frames are gathered in batches of --frames-per-gather on a rotating root (batch j on rank
-  j % N).  The frame-per-GPU weak-scaling number is reported beside it (`weak_scaling`).
+* N = 1: one step = one frame.  The value is the native frame loop (trt_render_frames: plain
+  frames go out as multi-frame launches) — `path` in the line says which path produced it; the
+  N > 1 path at one rank is reported beside it (`tiled_1gpu`) as the base of the scaling curve.
+* N > 1 (one process per GPU under torch.distributed.run): one step = N frames, EACH row-tiled
+  over all N GPUs (interleaved 8-row bands) and gathered over RCCL to its own root, rank i % N
+  (trt_render_multi_frames: per-frame rotating roots, so every device's xGMI links ingest at
+  once).  Per-GPU work per step is one frame's worth at every N ("scaling": "weak"); the strong
+  form (one frame per step over all N GPUs) and the frame-per-GPU form (no collective) are
+  reported beside it.
 
 Rank 0 prints ONE JSON line.  Extra keys: `tiled_frame` (BASELINE configs[3]: a 3840x2160
-~100k-triangle frame row-tiled over the N GPUs and gathered on rank 0 over RCCL, with its
-SHA-256 checked against the 1-GPU frame and the committed hash), `shipped_frame` (the
-reference's own default frame, config.hpp:97-101 at MAX_DEPTH 20), `readme_frame` (the scene
-of the reference's only published frame rate, README.md:334-340), `roofline` (FP32 VALU:
-SURVEY §8d flop units x this frame's counted work / the kernel's HIP-event launch time),
-`cpu_baseline` (the CPU oracle timed on this host on the same workload).
+~100k-triangle frame row-tiled over the N GPUs and gathered on rank 0 over RCCL, hash-checked
+against the 1-GPU frame and the committed hash), `shipped_frame` (the reference's own default
+frame, config.hpp:97-101 at MAX_DEPTH 20), `readme_frame` (the scene of the reference's only
+published frame rate, README.md:334-340), `roofline` (FP32 VALU: SURVEY §8d flop units x the
+counted work / wall time per frame), `cpu_baseline` (the CPU oracle on this host).
 """
 from __future__ import annotations
 
@@ -34,15 +39,16 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 # frames in flight are HIP streams: 32 hardware queues (HIP's default, 4, is what the box's
-# environment sets) before any HIP init in this process
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:
-    os.environ["GPU_MAX_HW_QUEUES"] = "32"
+# environment sets) before any HIP init in this process (TRT_KEEP_HW_QUEUES=1 opts out)
+from vkcomputeshader_tinyraytracer_amd._lib import raise_hw_queues  # noqa: E402
+
+raise_hw_queues()
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector, FMA = 2 flops (AMD spec)
-TIME_EVERY = 16  # one timed (event-bracketed) launch per 16 frames
 FRAME_HASHES = REPO / "tests" / "golden" / "frame_hashes.json"
 METRIC = "Mray/s (primary+secondary) at 1024×768 depth4; 1/2/4/8-GPU scaling"
+RING = 256  # output images of a timed loop (frame i -> image i % RING)
 
 
 def parse():
@@ -52,14 +58,16 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5", "ref", "readme"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget per thread count")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight (trt_set_frames_in_flight: 0 = auto = 4, or 8 for deferred-shadow "
-                         "frames; the reference's MAX_FRAMES_IN_FLIGHT is 2)")
+                    help="frames in flight (trt_set_frames_in_flight: 0 = auto; the reference's is 2)")
+    ap.add_argument("--frame-batch", type=int, default=0,
+                    help="frames per launch (trt_set_frame_batch: 0 = auto, 1 = one launch per frame)")
     ap.add_argument("--split", type=int, default=0, help="subtree split window (trt_set_subtree_split: 0 auto, 1 off)")
     ap.add_argument("--band-rows", type=int, default=8, help="rows per band of the tiled frames")
-    ap.add_argument("--frames-per-gather", type=int, default=64,
-                    help="frames whose bands move in one RCCL gather (N > 1 headline)")
+    ap.add_argument("--frames-per-gather", type=int, default=0,
+                    help="frames per RCCL exchange of the tiled loop (0 = auto: a quarter of the frames, <= 64)")
+    ap.add_argument("--camera-period", type=int, default=16, help="distinct camera positions of the walk")
     ap.add_argument("--tiled-frames", type=int, default=20,
                     help="frames of the tiled 3840x2160 leg (C4 row-tiled + RCCL gather on rank 0); 0 skips it")
     ap.add_argument("--extra-frames", type=int, default=40,
@@ -91,7 +99,7 @@ def make_scene(name: str):
 
 # ---- roofline units ---------------------------------------------------------
 
-def algorithmic_flops(st: dict, pixels: int, envmap: bool, mesh: bool) -> int:
+def algorithmic_flops(st: dict, envmap: bool, mesh: bool) -> int:
     """FP32 flops of the work the frame executes, in SURVEY §8(d) units: slab test 24 per box
     (BVH / hierarchy node or the reference's batch gate), Moller-Trumbore 22 / 34 / 52 / 59 by
     the stage it exits at (+27 for the hit's interpolated normal), sphere test 21, floor test 8,
@@ -106,7 +114,6 @@ def algorithmic_flops(st: dict, pixels: int, envmap: bool, mesh: bool) -> int:
     total = (24 * (st["node_tests"] + st["batch_tests"]) + mt + 27 * st["tri_nearest"]
              + 21 * st["sphere_tests"] + 8 * scene_queries + (3 * queries if mesh else 0)
              + 180 * hits + (40 * st["misses"] if envmap else 0))
-    # the counting pass traces the shadow queries the frame skips (zero contribution): not executed
     skipped = (24 * st["skipped_box_tests"] + 22 * st["skipped_tri_tests"] + 12 * st["skipped_tri_past_a"]
                + 18 * st["skipped_tri_past_u"] + 7 * st["skipped_tri_past_v"] + 21 * st["skipped_sphere_tests"]
                + (3 * st["shadow_skipped"] if mesh else 0))
@@ -123,31 +130,81 @@ def algorithmic_bytes(st: dict, pixels: int, envmap: bool) -> int:
                + (16 * st["misses"] if envmap else 0) + 84 * st["tri_nearest"] + 4 * pixels)
 
 
+def roofline(st_frame: dict, s_per_frame: float, envmap: bool, mesh: bool, pixels: int,
+             kernel_ms_per_frame: float | None = None) -> dict:
+    """FP32-VALU roofline of one frame's counted work over the wall time per frame (the wall
+    clock of the timed loop / frames — never more than the time the frames took)."""
+    flops = algorithmic_flops(st_frame, envmap, mesh)
+    tf = flops / s_per_frame / 1e12
+    out = {
+        "bound": "valu", "achieved": round(tf, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(tf / VALU_PEAK_TFLOPS, 4), "traffic": None,
+        "flops_per_frame": flops, "us_per_frame": round(s_per_frame * 1e6, 3),
+    }
+    if kernel_ms_per_frame is not None:
+        out["kernel_us_per_frame"] = round(kernel_ms_per_frame * 1e3, 3)
+        out["kernel_frac"] = round(flops / (kernel_ms_per_frame * 1e-3) / 1e12 / VALU_PEAK_TFLOPS, 4)
+    ab = algorithmic_bytes(st_frame, pixels, envmap)
+    out["hbm_index"] = {"algorithmic_bytes_per_frame": ab, "gb_s": round(ab / s_per_frame / 1e9, 2),
+                        "peak": HBM_PEAK_GBS}
+    return out
+
+
+def cpu_info() -> dict:
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+
+
 def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
-    """CPU oracle (fast mode) on this host: whole frames, 1 warm-up, median of >= 3 frames
-    within the time budget."""
+    """CPU oracle (fast mode, -O3, rows dynamically scheduled over pthreads) on this host, on
+    whole frames of the same workload (camera at the walk's start): at
+    std::thread::hardware_concurrency() threads (SURVEY §8d) and at the process's CPU share."""
     from oracle import oracle as orc
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 64))
-    orc.render(scene, params, threads=threads)  # warm-up (also loads/builds the library)
-    times = []
-    t_start = time.perf_counter()
-    while len(times) < 3 or (time.perf_counter() - t_start < budget_s and len(times) < 50):
-        t0 = time.perf_counter()
-        _, _, st = orc.render(scene, params, threads=threads)
-        times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    cpu_rays = st["primary_rays"] + st["secondary_rays"]
-    return {
-        "value": round(cpu_rays / med / 1e6, 3),
-        "unit": "Mray/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{len(times)} whole frames of the same workload after 1 warm-up, median "
-                  f"{med * 1e3:.1f} ms/frame; oracle/trt_oracle.c fast mode, -O3, rows over {threads} threads",
-        "rays_match_gpu": bool(cpu_rays == rays_per_frame),
+    info = cpu_info()
+    hw = min(os.cpu_count() or 1, 256)  # the oracle caps its pool at 256 threads
+    share = info["affinity_cpus"] or hw
+    if info["cgroup_cpu_quota"]:
+        share = min(share, max(1, int(info["cgroup_cpu_quota"])))
+
+    def run(threads):
+        orc.render(scene, params, threads=threads)  # warm-up (also loads/builds the library)
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 3 or (time.perf_counter() - t_start < budget_s and len(times) < 50):
+            t0 = time.perf_counter()
+            _, _, st = orc.render(scene, params, threads=threads)
+            times.append(time.perf_counter() - t0)
+        med = statistics.median(times)
+        return st["primary_rays"] + st["secondary_rays"], med, len(times)
+
+    rays, med, n = run(hw)
+    out = {
+        "value": round(rays / med / 1e6, 3), "unit": "Mray/s", "cores": hw, "kind": "port",
+        "sample": f"{n} whole frames of the same workload after 1 warm-up, median {med * 1e3:.1f} ms/frame; "
+                  f"oracle/trt_oracle.c fast mode, -O3, rows over {hw} threads (hardware_concurrency)",
+        "host": info, "rays_match_gpu": bool(rays == rays_per_frame),
     }
+    if share != hw:
+        r2, med2, n2 = run(share)
+        out["at_cpu_share"] = {"threads": share, "value": round(r2 / med2 / 1e6, 3), "frames": n2,
+                               "ms_per_frame": round(med2 * 1e3, 2)}
+    return out
 
 
 class Group:
@@ -169,6 +226,9 @@ class Group:
 
     def max(self, x: float) -> float:
         return self._reduce(x, "MAX")
+
+    def min(self, x: float) -> float:
+        return self._reduce(x, "MIN")
 
     def sum(self, x: float) -> float:
         return self._reduce(x, "SUM")
@@ -209,60 +269,156 @@ def timed(g: Group, fn) -> float:
     return g.max(time.perf_counter() - t0)
 
 
-def frame_loop(dev: int, scene, frames: int, warmup: int, inflight: int, split: int, time_every: int = TIME_EVERY,
-               g: Group | None = None):
-    """trt_render_frames of `scene` on one GPU: (elapsed s, kernel ms per sampled launch, stats of
-    a counting pass, params)."""
+def walk(scene, period: int):
+    from vkcomputeshader_tinyraytracer_amd import camera_path
+
+    return camera_path(scene.ubo, period)
+
+
+def count_walk(r, p, walk_ubos) -> tuple[list[dict], dict]:
+    """Counting pass of every camera position of the walk: (per-position stats, their mean)."""
+    per = []
+    for u in walk_ubos:
+        r.update_ubo(u)
+        _, _, st = r.draw_frame(p, count=True)
+        per.append(st)
+    mean = {k: sum(s[k] for s in per) / len(per) for k in per[0] if k != "kernel_ms"}
+    return per, mean
+
+
+def rays_of(st: dict) -> int:
+    return int(st["primary_rays"] + st["secondary_rays"])
+
+
+def frame_loop(dev: int, scene, frames: int, warmup: int, args, g: Group | None = None, check_last: bool = True):
+    """trt_render_frames of `scene` on one GPU over the camera walk: wall time, per-frame launch
+    times, the walk's counts, and whether the last timed frame equals trt_render of its UBO."""
+    import numpy as np
     import torch
 
     import vkcomputeshader_tinyraytracer_amd as trt
 
     p = scene.params()
+    wk = walk(scene, args.camera_period)
     r = trt.Renderer(dev)
     try:
         r.upload_scene(scene)
-        r.set_subtree_split(split)
-        _, _, st = r.draw_frame(p, count=True)  # counting pass, excluded from timing
-        out8 = torch.empty((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+        r.set_subtree_split(args.split)
+        per, mean = count_walk(r, p, wk)
+        rays_total = sum(rays_of(per[i % len(wk)]) for i in range(frames))
+        ring = min(frames, RING)
+        ubos = np.stack([wk[i % len(wk)] for i in range(frames)])
+        out8 = torch.empty((ring, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+        fb = p.height * p.width * 4
         stream = torch.cuda.Stream()
         r.set_stream(stream)
-        r.set_frames_in_flight(inflight)
-        r.render_frames(p, out8, warmup)
-        box = {}
-        elapsed = timed(g or Group(1, 0), lambda: box.update(n=r.render_frames(p, out8, frames, timing=True,
-                                                                                 time_every=time_every)))
-        kern_ms = r.frame_times(box["n"])
-        return elapsed, kern_ms, st, p
+        r.set_frames_in_flight(args.inflight)
+        r.set_frame_batch(args.frame_batch)
+        r.render_frames(p, out8, max(1, min(warmup, ring)), ubos=ubos, frame_stride=fb)
+        box = {"ms": [], "nf": []}
+
+        def run():
+            for i0 in range(0, frames, ring):
+                n = min(ring, frames - i0)
+                nt = r.render_frames(p, out8, n, ubos=ubos[i0:i0 + n], frame_stride=fb, timing=True)
+                box["ms"].append(r.frame_times(nt))
+                box["nf"].append(r.launch_frames())
+
+        elapsed = timed(g or Group(1, 0), run)
+        ms = np.concatenate(box["ms"])
+        nf = np.concatenate(box["nf"]).astype(np.float64)
+        kernel_ms_per_frame = float((ms * nf).sum() / nf.sum())  # launch spans / frames
+        launches = int(len(nf))
+        ok = None
+        if check_last:
+            last = frames - 1
+            got = out8[last % ring].cpu().numpy()
+            r.set_stream(None)
+            r.update_ubo(ubos[last])
+            want, _, _ = r.draw_frame(p)
+            ok = bool(np.array_equal(got, want))
+        return {"elapsed": elapsed, "rays_total": rays_total, "mean": mean, "p": p,
+                "kernel_ms_per_frame": kernel_ms_per_frame, "launches": launches, "last_frame_ok": ok}
     finally:
         r.close()
 
 
-def resolved_inflight(inflight: int, scene) -> int:
-    """The library's frames in flight for this scene: the explicit count, or its auto rule (8
-    for deferred-shadow frames: meshes at max_depth >= 8 and spp 1, else 4)."""
-    if inflight:
-        return inflight
-    return 8 if (len(scene.models) > 0 and scene.max_depth >= 8 and scene.spp <= 1) else 4
+def auto_per_gather(total: int, arg: int) -> int:
+    if arg > 0:
+        return arg
+    return max(1, min(64, -(-total // 4)))  # >= 4 exchanges pipeline in the timed region
+
+
+def tiled_loop(g: Group, dev: int, multi, scene, frames: int, warmup: int, args, per_gather: int, root: int):
+    """trt_render_multi_frames over all ranks along the camera walk: frame i row-tiled over the
+    ranks and assembled on rank frame_root(i): (elapsed s, rays of all frames, walk mean stats,
+    last-frame check on every rank that rooted frames)."""
+    import numpy as np
+    import torch
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+    from vkcomputeshader_tinyraytracer_amd.multi import frame_root
+
+    p = scene.params()
+    wk = walk(scene, args.camera_period)
+    multi.upload_scene(scene if g.rank == 0 else None)
+    per = []
+    for u in wk:  # counting passes (all ranks), excluded from timing
+        multi.update_ubo(u)
+        per.append(multi.draw_frame(p, band_rows=args.band_rows, root=0, count=True))
+    mean = {k: sum(s[k] for s in per) / len(per) for k in per[0] if k != "kernel_ms"}
+    rays_total = sum(rays_of(per[i % len(wk)]) for i in range(frames))
+    ring = min(frames, RING - RING % g.world)  # a multiple of the ranks: frame i keeps root i % N
+    ubos = np.stack([wk[i % len(wk)] for i in range(frames)])
+    fb = p.height * p.width * 4
+    out = torch.zeros((ring, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    multi.set_stream(0, stream)
+    # warmup: one exchange of the timed size, so the timed batches never allocate
+    multi.render_frames(p, max(min(warmup, ring), min(per_gather, ring)), args.band_rows, root, per_gather,
+                        outs=[out], frame_stride=fb, ubos=ubos)
+
+    def run():
+        for i0 in range(0, frames, ring):
+            n = min(ring, frames - i0)
+            multi.render_frames(p, n, args.band_rows, root, per_gather, outs=[out], frame_stride=fb,
+                                ubos=ubos[i0:i0 + n])
+
+    elapsed = timed(g, run)
+    multi.set_stream(0, None)
+    # the last frame this rank assembled vs trt_render of its UBO on this GPU
+    mine = [i for i in range(frames) if frame_root(i % ring, g.world, root) == g.rank]
+    ok = 1.0
+    if mine:
+        last = mine[-1]
+        got = out[last % ring].cpu().numpy()
+        with trt.Renderer(dev) as r:
+            r.upload_scene(scene)
+            r.update_ubo(ubos[last])
+            want, _, _ = r.draw_frame(p)
+        ok = 1.0 if np.array_equal(got, want) else 0.0
+    ok = g.min(ok)
+    return elapsed, rays_total, mean, bool(ok > 0.5)
 
 
 def extra_frame(dev: int, name: str, frames: int, args) -> dict:
-    import vkcomputeshader_tinyraytracer_amd  # noqa: F401  (lib load)
-
     sc = make_scene(name)
-    elapsed, kern_ms, st, p = frame_loop(dev, sc, frames, 4, args.inflight, args.split, time_every=4)
-    rays = st["primary_rays"] + st["secondary_rays"]
-    ms = elapsed / frames * 1e3
+    res = frame_loop(dev, sc, frames, 4, args)
+    ms = res["elapsed"] / frames * 1e3
+    mean = res["mean"]
+    p = res["p"]
     out = {
-        "workload": f"{name}: {WORKLOADS[name]}",
+        "workload": f"{name}: {WORKLOADS[name]}; camera walk of {args.camera_period} positions",
         "frames": frames,
-        "frames_in_flight": resolved_inflight(args.inflight, sc),
         "ms_per_frame": round(ms, 4),
         "fps": round(1e3 / ms, 2),
-        "mray_s": round(rays / (ms * 1e-3) / 1e6, 3),
-        "rays_per_frame": rays,
-        "shadow_rays_per_frame": st["shadow_rays"],
-        "shadow_rays_traced_per_frame": st["shadow_rays"] - st["shadow_skipped"],
-        "kernel_span_ms": round(float(kern_ms.mean()), 4),
+        "mray_s": round(res["rays_total"] / res["elapsed"] / 1e6, 3),
+        "rays_per_frame": round(res["rays_total"] / frames, 1),
+        "shadow_rays_per_frame": round(mean["shadow_rays"], 1),
+        "shadow_rays_traced_per_frame": round(mean["shadow_rays"] - mean["shadow_skipped"], 1),
+        "launches": res["launches"],
+        "last_frame_matches_trt_render": res["last_frame_ok"],
+        "roofline": roofline(mean, ms * 1e-3, True, True, p.width * p.height, res["kernel_ms_per_frame"]),
     }
     if name == "readme":
         out["published_context"] = {
@@ -274,37 +430,26 @@ def extra_frame(dev: int, name: str, frames: int, args) -> dict:
     return out
 
 
-def tiled_stream(g: Group, dev: int, multi, scene, frames: int, warmup: int, band_rows: int, root: int,
-                 per_gather: int):
-    """trt_render_multi_frames of `scene` over all ranks: (elapsed s, whole-frame stats, output)."""
-    import torch
-
-    p = scene.params()
-    multi.upload_scene(scene if g.rank == 0 else None)
-    st = multi.draw_frame(p, band_rows=band_rows, root=0, count=True)  # counting pass (all ranks)
-    out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.Stream()
-    multi.set_stream(0, stream)
-    # warmup: at least one batch of the timed batches' size, so the gather buffers are sized
-    # before timing (the timed batches never allocate)
-    multi.render_frames(p, max(warmup, min(frames, per_gather)), band_rows, root, per_gather, outs=[out])
-    elapsed = timed(g, lambda: multi.render_frames(p, frames, band_rows, root, per_gather, outs=[out]))
-    multi.set_stream(0, None)
-    return elapsed, st, out, p
-
-
-def tiled_frame(g: Group, dev: int, multi, frames: int, band_rows: int) -> dict:
+def tiled_frame(g: Group, dev: int, multi, frames: int, args) -> dict | None:
     """BASELINE configs[3]: a 3840x2160 C4 frame row-tiled across the ranks (interleaved
     band_rows-row bands) and gathered to rank 0 as RGBA8 over RCCL (xGMI) by the native path,
-    one gather per frame (the display case), two frames in flight."""
+    one exchange per frame (the display case)."""
     import torch
 
     import vkcomputeshader_tinyraytracer_amd as trt
     from vkcomputeshader_tinyraytracer_amd import scene as S
 
     sc = S.config_c4()
-    elapsed, st, out, p = tiled_stream(g, dev, multi, sc, frames, 2, band_rows, 0, 1)
-    rays = st["primary_rays"] + st["secondary_rays"]
+    p = sc.params()
+    multi.upload_scene(sc if g.rank == 0 else None)
+    st = multi.draw_frame(p, band_rows=args.band_rows, root=0, count=True)
+    out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    multi.set_stream(0, stream)
+    multi.render_frames(p, 2, args.band_rows, 0, 1, outs=[out])
+    elapsed = timed(g, lambda: multi.render_frames(p, frames, args.band_rows, 0, 1, outs=[out]))
+    multi.set_stream(0, None)
+    rays = rays_of(st)
     res = None
     if g.rank == 0:
         sha = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
@@ -313,14 +458,16 @@ def tiled_frame(g: Group, dev: int, multi, frames: int, band_rows: int) -> dict:
             one, _, _ = r.draw_frame(p)
         sha1 = hashlib.sha256(one.tobytes()).hexdigest()
         committed = json.loads(FRAME_HASHES.read_text()).get("C4_3840x2160") if FRAME_HASHES.exists() else None
+        ms = elapsed / frames * 1e3
         res = {
             "workload": "C4: 3840x2160, 20 icospheres (102,400 tris), depth 4, one frame row-tiled "
-                        f"over {g.world} GPU(s) in interleaved {band_rows}-row bands, gathered on rank 0",
+                        f"over {g.world} GPU(s) in interleaved {args.band_rows}-row bands, gathered on rank 0",
             "scaling": "strong",
-            "collective": "RCCL grouped ncclSend/ncclRecv of the compact RGBA8 band buffers to rank 0 "
-                          "(csrc/trt_multi.cpp)" + (" — 1 rank: sent to itself" if g.world == 1 else ""),
+            "collective": ("RCCL grouped ncclSend/ncclRecv of the compact RGBA8 band buffers to rank 0 "
+                           "(csrc/trt_multi.cpp, plan csrc/band_plan.cpp)") if g.world > 1 else
+                          "none at 1 rank: rank 0 traces every band in place, nothing travels",
             "frames": frames,
-            "ms_per_frame": round(elapsed / frames * 1e3, 4),
+            "ms_per_frame": round(ms, 4),
             "frames_per_s": round(frames / elapsed, 3),
             "mray_s": round(rays * frames / elapsed / 1e6, 3),
             "rays_per_frame": rays,
@@ -328,9 +475,22 @@ def tiled_frame(g: Group, dev: int, multi, frames: int, band_rows: int) -> dict:
             "frame_sha256": sha,
             "matches_1gpu_frame": sha == sha1,
             "matches_committed_hash": (sha == committed) if committed else None,
+            "committed_hash_note": "regression check: the committed hash is this kernel's own earlier output, "
+                                   "not an independent reference (C4 parity vs the oracle: tests/test_gpu_fullres.py)",
+            "roofline": roofline(st, ms * 1e-3, True, True, p.width * p.height),
         }
     torch.cuda.synchronize()
     return res
+
+
+def count_first(dev: int, scene) -> dict:
+    """Counting pass of the scene's own UBO (the camera the CPU baseline renders)."""
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    with trt.Renderer(dev) as r:
+        r.upload_scene(scene)
+        _, _, st = r.draw_frame(scene.params(), count=True)
+    return st
 
 
 def main():
@@ -344,7 +504,6 @@ def main():
     dev = torch.cuda.current_device()
     g = Group(world, rank)
 
-    import vkcomputeshader_tinyraytracer_amd as trt
     from vkcomputeshader_tinyraytracer_amd import types as T
     from vkcomputeshader_tinyraytracer_amd.multi import ROOT_ROTATE, MultiRenderer
 
@@ -352,44 +511,54 @@ def main():
     K = args.steps
     envmap = bool(scene.flags & T.FLAG_ENVMAP)
     mesh = len(scene.models) > 0
+    pixels = scene.width * scene.height
 
-    # Frame per GPU (the N = 1 headline; the weak-scaling extra at N > 1): also the live kernel
-    # timing of the roofline.
-    elapsed1, kern_ms, st, params = frame_loop(dev, scene, K, args.warmup, args.inflight, args.split, g=g)
-    rays_per_frame = st["primary_rays"] + st["secondary_rays"]
-    pixels = params.width * params.height
-    kern_avg_ms = g.max(float(kern_ms.mean()))
-    weak_value = g.sum(rays_per_frame) * K / elapsed1 / 1e6
+    # Frame per GPU: the plain frame loop on every rank, no data-path collective (the N = 1
+    # value; at N > 1 the frame-per-GPU extra).  Also the live launch timing.
+    fl = frame_loop(dev, scene, K, args.warmup, args, g=g)
+    plain_value = g.sum(fl["rays_total"]) / fl["elapsed"] / 1e6
+    plain_ok = g.min(1.0 if fl["last_frame_ok"] else 0.0) > 0.5
 
     multi = MultiRenderer.for_rank(dev, world, rank, g.unique_id())
+    # the tiled loop: N frames per step (weak), each row-tiled over all N GPUs, rotating roots
+    t_frames = K * world
+    fpg = auto_per_gather(t_frames, args.frames_per_gather)
+    el_t, rays_t, mean_t, tiled_ok = tiled_loop(g, dev, multi, scene, t_frames, args.warmup, args, fpg, ROOT_ROTATE)
+    tiled_value = rays_t / el_t / 1e6
+    tiled = {
+        "value": round(tiled_value, 3), "unit": "Mray/s", "ms_per_step": round(el_t / K * 1e3, 5),
+        "frames": t_frames, "frames_per_gather": fpg, "last_frames_match_trt_render": tiled_ok,
+        "path": "trt_render_multi_frames: every frame row-tiled over all ranks in interleaved "
+                f"{args.band_rows}-row bands, RCCL exchange of {fpg} frames per op to per-frame rotating roots "
+                "(frame i -> rank i % N)" + (" — 1 rank: every band traced in place, nothing travels"
+                                             if world == 1 else ""),
+    }
+    extra = {}
     if world == 1:
-        value, ms_per_step = weak_value, elapsed1 / K * 1e3
-        scaling, parallelism = "weak", "1 GPU"
-        # the N > 1 headline's path (trt_render_multi_frames) at one rank: the base of its
-        # strong-scaling curve, so the driver's per-N values can be read against it
-        elapsed_t, mst, _, _ = tiled_stream(g, dev, multi, scene, K, args.warmup, args.band_rows, ROOT_ROTATE,
-                                            args.frames_per_gather)
-        rays_whole = mst["primary_rays"] + mst["secondary_rays"]
-        headline_extra = {"tiled_headline_1gpu": {
-            "value": round(rays_whole * K / elapsed_t / 1e6, 3), "unit": "Mray/s",
-            "ms_per_step": round(elapsed_t / K * 1e3, 5),
-            "workload": f"the N > 1 headline's path at 1 rank: {args.config} through trt_render_multi_frames "
-                        f"({args.band_rows}-row bands, RCCL gather of {args.frames_per_gather} frames per op)"}}
+        value, ms_per_step, scaling = plain_value, fl["elapsed"] / K * 1e3, "weak"
+        path = "trt_render_frames (plain frame loop, multi-frame launches)"
+        parallelism = "1 GPU"
+        extra["tiled_1gpu"] = dict(tiled, note="the N > 1 headline's path at one rank: the base of the scaling curve")
+        st_frame, s_frame = fl["mean"], fl["elapsed"] / K
     else:
-        # the frame row-tiled over all GPUs, RCCL gathers of --frames-per-gather frames on a rotating root
-        elapsed, mst, _, _ = tiled_stream(g, dev, multi, scene, K, args.warmup, args.band_rows, ROOT_ROTATE,
-                                          args.frames_per_gather)
-        rays_whole = mst["primary_rays"] + mst["secondary_rays"]
-        value, ms_per_step = rays_whole * K / elapsed / 1e6, elapsed / K * 1e3
-        scaling = "strong"
-        parallelism = (f"row-tiled x{world} ({args.band_rows}-row interleaved bands), RCCL gather of "
-                       f"{args.frames_per_gather} frames per op on a rotating root")
-        headline_extra = {"weak_scaling": {
-            "value": round(weak_value, 3), "unit": "Mray/s",
-            "workload": f"frame per GPU: every rank renders its own whole {args.config} frame, no data-path collective",
-            "ms_per_step": round(elapsed1 / K * 1e3, 5)}}
+        value, ms_per_step, scaling = tiled_value, el_t / K * 1e3, "weak"
+        path = tiled["path"]
+        parallelism = (f"{world} frames per step, each row-tiled x{world} ({args.band_rows}-row interleaved bands), "
+                       "RCCL exchange to per-frame rotating roots")
+        extra["frame_per_gpu"] = {
+            "value": round(plain_value, 3), "unit": "Mray/s", "ms_per_step": round(fl["elapsed"] / K * 1e3, 5),
+            "workload": f"every rank renders its own whole {args.config} frames, no data-path collective",
+            "last_frame_ok": plain_ok}
+        # strong form: one frame per step over all N GPUs
+        fpg1 = auto_per_gather(K, args.frames_per_gather)
+        el_s, rays_s, _, ok_s = tiled_loop(g, dev, multi, scene, K, args.warmup, args, fpg1, ROOT_ROTATE)
+        extra["strong_scaling"] = {
+            "value": round(rays_s / el_s / 1e6, 3), "unit": "Mray/s", "ms_per_step": round(el_s / K * 1e3, 5),
+            "frames": K, "frames_per_gather": fpg1, "last_frames_match_trt_render": ok_s,
+            "workload": "one frame per step, row-tiled over all ranks (total work fixed as N grows)"}
+        st_frame, s_frame = mean_t, el_t / t_frames * world  # per-GPU wall time per frame of work
 
-    tiled = tiled_frame(g, dev, multi, args.tiled_frames, args.band_rows) if args.tiled_frames > 0 else None
+    tiled_c4 = tiled_frame(g, dev, multi, args.tiled_frames, args) if args.tiled_frames > 0 else None
     multi.close()
 
     extras = {}
@@ -406,9 +575,14 @@ def main():
             g.barrier()
 
     if rank == 0:
-        flops = algorithmic_flops(st, pixels, envmap, mesh)
-        tflops = flops / (kern_avg_ms * 1e-3) / 1e12
-        abytes = algorithmic_bytes(st, pixels, envmap)
+        rl = roofline(st_frame, s_frame, envmap, mesh, pixels, fl["kernel_ms_per_frame"] if world == 1 else None)
+        rl["kernel"] = "trace_kernel"
+        rl["note"] = ("FP32 flops of one frame's executed work in SURVEY §8d units (counting passes of the camera "
+                      "walk, mean per frame) / the wall time per frame of the timed loop (at N > 1: per GPU); "
+                      "kernel_us_per_frame = HIP-event span of every launch / the frames it traced (one launch "
+                      "traces many frames).  Peak counts an FMA as 2 flops; the kernel has no FMA contraction "
+                      "(-ffp-contract=off).  traffic: no PMC pass in this run (profiles/ holds this build's PMC "
+                      "summaries)")
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -421,54 +595,32 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded procedural envmap; reference spheres/lights/materials, main.cpp:125-143)",
+            "data": "synthetic (seeded procedural envmap; reference spheres/lights/materials, main.cpp:125-143; "
+                    f"camera walk of {args.camera_period} positions, main.cpp:391-403)",
+            "path": path,
             "config": {
                 "workload": f"{args.config}: {WORKLOADS[args.config]}",
-                "width": params.width,
-                "height": params.height,
-                "max_depth": params.max_depth,
-                "spp": params.spp,
-                "rays_per_frame": rays_per_frame,
-                "shadow_rays_per_frame": st["shadow_rays"],
-                "shadow_rays_traced_per_frame": st["shadow_rays"] - st["shadow_skipped"],
+                "width": scene.width,
+                "height": scene.height,
+                "max_depth": scene.max_depth,
+                "spp": scene.spp,
+                "rays_per_frame": round(fl["rays_total"] / K, 1),
+                "shadow_rays_per_frame": round(fl["mean"]["shadow_rays"], 1),
+                "shadow_rays_traced_per_frame": round(fl["mean"]["shadow_rays"] - fl["mean"]["shadow_skipped"], 1),
                 "parallelism": parallelism,
-                "frames_in_flight": resolved_inflight(args.inflight, scene),
+                "frames_per_step": world,
+                "launches": fl["launches"],
+                "last_frame_matches_trt_render": plain_ok if world == 1 else tiled_ok,
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(tflops, 3),
-                "peak": VALU_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(tflops / VALU_PEAK_TFLOPS, 4),
-                "traffic": None,
-                "kernel": "trace_kernel",
-                "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
-                "flops_per_launch": flops,
-                "achieved_per_frame": round(flops / (elapsed1 / K) / 1e12, 3),
-                "frac_per_frame": round(flops / (elapsed1 / K) / 1e12 / VALU_PEAK_TFLOPS, 4),
-                "note": "FP32 flops of the executed work in SURVEY §8d units (counting pass of this frame) / "
-                        "the trace kernel's launch time (HIP events on its stream, every 16th launch of the "
-                        "timed loop; with several frames in flight a launch's span includes the overlapping "
-                        "frames, so *_per_frame divides by the wall time per frame instead); "
-                        "peak counts an FMA as 2 flops, the kernel has no FMA contraction (-ffp-contract=off). "
-                        "traffic: no PMC pass in this run (profiles/ holds the PMC summaries of this build)",
-                "hbm_index": {
-                    "algorithmic_bytes_per_launch": abytes,
-                    "gb_s_per_launch": round(abytes / (kern_avg_ms * 1e-3) / 1e9, 2),
-                    "gb_s_per_frame": round(abytes / (elapsed1 / K) / 1e9, 2),
-                    "peak": HBM_PEAK_GBS,
-                    "note": "SURVEY §8d bytes excluding SGPR-resident sphere records and constant materials; "
-                            "an index, not measured traffic",
-                },
-            },
+            "roofline": rl,
         }
-        if headline_extra:
-            result.update(headline_extra)
-        if tiled is not None:
-            result["tiled_frame"] = tiled
+        result.update(extra)
+        if tiled_c4 is not None:
+            result["tiled_frame"] = tiled_c4
         result.update(extras)
         if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(scene, params, rays_per_frame, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(scene, scene.params(), rays_of(count_first(dev, scene)),
+                                                  args.cpu_seconds)
         print(json.dumps(result), flush=True)
     g.close()
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define TRT_ABI_VERSION 2
+#define TRT_ABI_VERSION 3
 
 /* status codes */
 #define TRT_OK 0
@@ -152,12 +152,26 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 8], or 0 = auto
  * (the default): 4, or 8 for deferred-shadow frames, whose depth-20 trees leave the longest
  * tails (measured: profiles/r02_ab_queues_*.log).  Each slot is a HIP stream, so the process
- * needs as many hardware queues: trt_create sets GPU_MAX_HW_QUEUES=32 in the environment when
- * it is unset and HIP is not yet initialised (HIP's default is 4). */
+ * needs as many hardware queues: the library leaves GPU_MAX_HW_QUEUES to the host (HIP's
+ * default is 4; the Python package and bench.py raise it to 32 before HIP initialises, see
+ * INTEGRATION.md). */
 #define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
 #define TRT_FRAMES_IN_FLIGHT_AUTO 0u
 #define TRT_MAX_FRAMES_IN_FLIGHT 8u
 int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
+
+/* Frames per launch of trt_render_frames.  The reference records one vkCmdDispatch per frame
+ * (main.cpp:2122-2124).  Here consecutive frames of a plain frame loop (no subtree split, no
+ * deferred shadows) whose UBOs differ only in camPos — the reference's interactive loop moves
+ * only the camera, main.cpp:391-403 — are traced by ONE launch of ntiles x n workgroups: frame
+ * k of the launch owns blocks [k * ntiles, (k + 1) * ntiles), so a frame's slowest tiles overlap
+ * the next frame's tiles inside one grid and the GPU drains once per launch instead of once per
+ * frame.  n in [1, TRT_MAX_FRAME_BATCH]: 1 = one launch per frame (the reference's dispatch per
+ * frame); 0 = auto (the default): up to TRT_MAX_FRAME_BATCH frames per launch.  Split and
+ * deferred-shadow frames always launch one frame at a time (per-frame scratch). */
+#define TRT_FRAME_BATCH_AUTO 0u
+#define TRT_MAX_FRAME_BATCH 64u
+int trt_set_frame_batch(trt_ctx* ctx, uint32_t n);
 
 /* Subtree split (load balance of deep refraction trees).  The reference traces a pixel's whole
  * Whitted tree depth-first in one invocation (shader.comp:423-583); in mesh scenes at depth 20
@@ -204,23 +218,26 @@ int trt_defer_stats(trt_ctx* ctx, uint32_t slot, uint64_t out[5]);
 
 /* The reference's frame loop (mainLoop -> drawFrame, main.cpp:405-438, 2181-2205) in one
  * call: for each of `nframes` frames, updateUniformBuffer with ubos[i] (or the current UBO
- * when ubos is NULL) and enqueue one trace launch writing out_rgba8 + i * frame_stride
- * bytes.  Frames in flight (above) may run concurrently: give concurrent frames distinct
- * images (frame_stride >= rows*width*4) unless they are identical — frame_stride 0 makes
- * every frame write the same image, like the reference's single storage image (binding 3,
- * main.cpp:865-926).  Requires TRT_FLAG_DEVICE_PTRS; only enqueues; all frames have
- * completed on the context's stream when work enqueued after the call runs.  Host cost per
- * frame is one kernel launch.  With TRT_FLAG_TIMING a HIP event pair brackets the launch of
- * every `time_every`-th frame (0 or 1: every frame) on its slot's stream (the span includes
- * any overlap with the other slots' frames) — an event pair costs a few microseconds of
- * queue time, so a sparse sample keeps a timed frame loop representative;
- * trt_frame_times() reads the sampled kernel times. */
+ * when ubos is NULL) and trace the frame into out_rgba8 + i * frame_stride bytes.  Plain
+ * frames are traced several per launch (trt_set_frame_batch); launches rotate over the
+ * frames-in-flight streams (trt_set_frames_in_flight), so frames may run concurrently: give
+ * concurrent frames distinct images (frame_stride >= rows*width*4) unless they are identical —
+ * frame_stride 0 makes every frame write the same image, like the reference's single storage
+ * image (binding 3, main.cpp:865-926).  Requires TRT_FLAG_DEVICE_PTRS; only enqueues; all
+ * frames have completed on the context's stream when work enqueued after the call runs.  With
+ * TRT_FLAG_TIMING a HIP event pair brackets every `time_every`-th launch (0 or 1: every
+ * launch) on its stream (the span includes any overlap with launches on the other streams);
+ * trt_frame_times() reads them. */
 int trt_render_frames(trt_ctx* ctx, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
                       uint8_t* out_rgba8, size_t frame_stride, uint32_t time_every);
 
-/* Device times (ms) of the frames sampled by the last timed trt_render_frames call (waits
- * for them); n <= the number of sampled frames. */
+/* Device time per frame (ms) of each launch timed by the last timed trt_render_frames call:
+ * the launch's event span divided by the frames it traced (waits for them); n <= the number
+ * of timed launches, trt_timed_launches(). */
 int trt_frame_times(trt_ctx* ctx, float* ms, uint32_t n);
+/* Launches timed by the last timed trt_render_frames call, and (frames_out, may be NULL) the
+ * frames each traced. */
+uint32_t trt_timed_launches(trt_ctx* ctx, uint32_t* frames_out, uint32_t cap);
 
 /* Waits for all work enqueued on the context's stream. */
 int trt_synchronize(trt_ctx* ctx);
@@ -246,8 +263,8 @@ void trt_params_default(trt_params* p);
 typedef struct trt_multi trt_multi;
 
 #define TRT_MULTI_ID_BYTES 128 /* ncclUniqueId */
-#define TRT_ROOT_ROTATE (-1)   /* root of frame batch j = rank j % ranks (spreads the gathers'
-                                  ingest over every device's xGMI links) */
+#define TRT_ROOT_ROTATE (-1)   /* root of frame i = rank i % ranks (every device's xGMI links
+                                  ingest frames at once) */
 
 /* One process drives `ndev` devices (ncclCommInitAll); rank i = devices[i]. */
 int trt_multi_create(trt_multi** out, const int* devices, uint32_t ndev);
@@ -277,15 +294,62 @@ int trt_multi_update_ubo(trt_multi* m, const trt_ubo* ubo);
 int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int root,
                      uint8_t* const* out_rgba8, trt_stats* st);
 /* The frame loop of trt_render_frames, tiled: frames i = 0..nframes-1 (UBO ubos[i], or the
- * current one) in batches of `frames_per_gather` frames whose band buffers move in ONE grouped
- * gather; frame i lands at out_rgba8[root's local index] + i * frame_stride.  Two batches are
- * in flight: a batch's gather + re-interleave overlaps the next batch's render.  Requires
- * TRT_FLAG_DEVICE_PTRS; only enqueues (complete on each context's stream).  Collective. */
+ * current one) in batches of `frames_per_gather` frames.  Each device traces its band groups of
+ * a batch's frames (multi-frame launches, trt_set_frame_batch), then ONE grouped ncclSend /
+ * ncclRecv moves every frame's bands to that frame's root (trt_band_plan) and each root
+ * re-interleaves its frames: frame i lands at out_rgba8[local index of its root] + i *
+ * frame_stride on rank trt_frame_root(i, ranks, root) — with TRT_ROOT_ROTATE frame i goes to rank
+ * i % ranks, so every device ingests at once and every rank's entry must be set; with a fixed
+ * root only the root's entry is written.  Two batches are in flight: a batch's gather +
+ * re-interleave overlaps the next batch's render.  Requires TRT_FLAG_DEVICE_PTRS; only
+ * enqueues (complete on each context's stream).  Collective. */
 int trt_render_multi_frames(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
                             uint32_t band_rows, int root, uint32_t frames_per_gather,
                             uint8_t* const* out_rgba8, size_t frame_stride);
 /* Waits for every context stream of this process. */
 int trt_multi_synchronize(trt_multi* m);
+/* Test / diagnostic: with on != 0 the root's own band groups also travel through the gather
+ * (an ncclSend to itself and the re-interleave) instead of being rendered in place, so the
+ * whole exchange runs on a one-GPU communicator.  Same image; slower. */
+int trt_multi_set_self_gather(trt_multi* m, int on);
+
+/* ---- the exchange plan of a tiled batch ---------------------------------------------------
+ * The data movement trt_render_multi_frames performs for a batch of `nframes` frames starting
+ * at frame `first_frame` of the call, as a list of transfers, so a host with its own transport
+ * (MPI, torch.distributed, ...) can run the same exchange; trt_multi.cpp executes exactly this
+ * plan over RCCL (ncclSend / ncclRecv in list order on both ends, one group).  Frame i's root is
+ * trt_frame_root(i, nranks, root): `root`, or i % nranks for TRT_ROOT_ROTATE.  Rank r renders
+ * band groups r * groups_per_rank .. + groups_per_rank - 1 of every frame; a group's rows
+ * of frame f are stored compactly at (f * groups_per_rank + v) * block_bytes of the rank's
+ * batch buffer; a root receives them at (j * groups + g) * block_bytes of its gather buffer, j
+ * = the frame's index among the batch frames it roots; then compact row k of group g is frame
+ * row trt_band_frame_row(k, band_rows, groups, g).  Without TRT_PLAN_SELF_GATHER the root's own
+ * groups do not travel (it renders them in place).  Pure host arithmetic (no GPU). */
+typedef struct trt_band_layout {
+    uint32_t groups;       /* band groups NG = nranks * groups_per_rank */
+    uint32_t max_rows;     /* compact rows of the largest group */
+    uint64_t block_bytes;  /* one compact group buffer: max_rows * width * 4 */
+    uint64_t local_bytes;  /* a rank's batch buffer: nframes * groups_per_rank * block_bytes */
+    uint64_t gather_bytes; /* the largest gather buffer of a root: frames rooted * groups * block_bytes */
+} trt_band_layout;
+typedef struct trt_band_xfer {
+    uint32_t frame;      /* frame of the batch (0 .. nframes-1) */
+    uint32_t group;      /* global band group */
+    uint32_t src, dst;   /* sending rank (group / groups_per_rank), receiving rank (the frame's root) */
+    uint32_t rows;       /* compact rows of the group */
+    uint32_t slot;       /* the frame's index among the batch frames `dst` roots */
+    uint64_t src_offset; /* bytes into the sender's batch buffer */
+    uint64_t dst_offset; /* bytes into the root's gather buffer */
+    uint64_t bytes;      /* rows * width * 4 */
+} trt_band_xfer;
+#define TRT_PLAN_SELF_GATHER 1u
+uint32_t trt_frame_root(uint32_t frame, uint32_t nranks, int root);
+uint32_t trt_band_frame_row(uint32_t k, uint32_t band_rows, uint32_t groups, uint32_t g);
+/* Fills *layout and up to `cap` transfers (xfers may be NULL to count them); *count = the
+ * number of transfers of the plan. */
+int trt_band_plan(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks, uint32_t groups_per_rank,
+                  uint32_t first_frame, uint32_t nframes, int root, uint32_t flags, trt_band_layout* layout,
+                  trt_band_xfer* xfers, uint32_t cap, uint32_t* count);
 
 /* ---- host scene build (main.cpp:192-252, 1529-1580, 2290-2335) -------------------- */
 

@@ -1,5 +1,12 @@
-"""Shared comparison helpers for the parity tests."""
+"""Shared comparison helpers for the parity tests.
+
+With TRT_PARITY_LOG=<path> every comparison appends one JSON line (test id, max |d|,
+differing-pixel fraction, max float error) to <path>: the measured use of the parity bar
+(profiles/r03_parity_log.jsonl, summarised in DESIGN.md §2)."""
 from __future__ import annotations
+
+import json
+import os
 
 import numpy as np
 
@@ -13,6 +20,8 @@ import numpy as np
 #    full scale before gamma, <= 2.2x that after.  5e-3 (~1.3 LSB of 8-bit) bounds it.
 RGBA8_TOL = 1
 FLOAT_TOL = 5e-3
+# Largest fraction of pixels allowed to differ (by at most RGBA8_TOL).
+MAX_FRAC = 0.02
 
 
 def diff_report(a8: np.ndarray, b8: np.ndarray) -> dict:
@@ -24,9 +33,19 @@ def diff_report(a8: np.ndarray, b8: np.ndarray) -> dict:
     }
 
 
-def assert_rgba8_close(gpu: np.ndarray, ref: np.ndarray, tol: int = RGBA8_TOL, max_frac: float = 0.02):
+def _log(kind: str, rep: dict) -> None:
+    path = os.environ.get("TRT_PARITY_LOG")
+    if not path:
+        return
+    rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "?").rsplit(" ", 1)[0], "kind": kind, **rep}
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
+def assert_rgba8_close(gpu: np.ndarray, ref: np.ndarray, tol: int = RGBA8_TOL, max_frac: float = MAX_FRAC):
     assert gpu.shape == ref.shape, (gpu.shape, ref.shape)
     rep = diff_report(gpu, ref)
+    _log("rgba8", dict(rep, px=int(np.prod(gpu.shape[:-1]))))
     assert rep["max"] <= tol, f"RGBA8 mismatch beyond {tol} LSB: {rep}"
     assert rep["frac_px_diff"] <= max_frac, f"too many differing pixels: {rep}"
     assert (gpu[..., 3] == 255).all()
@@ -37,5 +56,6 @@ def assert_float_close(gpu: np.ndarray, ref: np.ndarray, tol: float = FLOAT_TOL)
     assert gpu.shape == ref.shape
     d = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
     assert np.isfinite(gpu).all()
+    _log("float", {"max_abs": float(d.max()) if d.size else 0.0})
     assert d.max() <= tol, f"float mismatch {d.max()} > {tol}"
     return float(d.max())

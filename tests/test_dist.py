@@ -1,9 +1,16 @@
-"""Multi-process frame tiling on the CPU (gloo, world sizes 2 and 3): row-band assignment,
-the gather to rank 0 and the re-interleave give exactly the single-process frame.  The CPU
-oracle stands in for the per-rank HIP render here (the GPU path is the same TiledFrame with
-hip_render_fn, exercised by tests/test_gpu_dist.py)."""
+"""The tiled path's partition and exchange with more than one rank, on the CPU.
+
+The native multi-GPU path (csrc/trt_multi.cpp) runs the exchange plan of `trt_band_plan`
+(csrc/band_plan.cpp) over RCCL; dist.TiledFrames runs the same plan — the same C function,
+same transfers, offsets and row mapping — over torch.distributed.  Here world sizes 2 and 3
+(gloo, spawned processes) render their band groups with the CPU oracle, exchange them per the
+plan and assemble every frame on its root (rotating per frame, or fixed); each frame must equal
+the oracle's whole frame bit for bit.  The plan's own invariants (every row of
+every frame delivered exactly once, buffers in bounds, no overlaps) are checked directly for
+the 8-GPU shapes the bench uses."""
 from __future__ import annotations
 
+import ctypes
 import os
 import socket
 
@@ -15,6 +22,7 @@ import torch.multiprocessing as mp
 
 from vkcomputeshader_tinyraytracer_amd import dist as D
 from vkcomputeshader_tinyraytracer_amd import types as T
+from vkcomputeshader_tinyraytracer_amd.multi import ROOT_ROTATE, band_frame_row, band_plan, frame_root
 
 
 def _free_port() -> int:
@@ -23,7 +31,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, band_rows, W, H, q):
+def _worker(rank, world, port, band_rows, groups, root, nframes, W, H, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -32,38 +40,59 @@ def _worker(rank, world, port, band_rows, W, H, q):
         from vkcomputeshader_tinyraytracer_amd import scene as S
 
         sc = S.config_c2(W, H, env_size=(256, 128))
-        tf = D.TiledFrame(W, H, band_rows=band_rows)
-        p = D.band_params(sc.params(), band_rows, world, rank)
+        ubos = np.stack([S.make_ubo(cam=(0.1 * i, 0.0, -0.15 * i)) for i in range(nframes)])
 
-        def render_fn(out):
-            img, _, _ = orc.render(sc, p, threads=2)
-            out[: img.shape[0]] = torch.from_numpy(img)
+        def render_fn(frame, g, p, out):
+            s2 = S.Scene(sc.name, ubos[frame], sc.tris, sc.models, sc.env, flags=sc.flags,
+                         max_depth=sc.max_depth)
+            img, _, _ = orc.render(s2, p, threads=2)
+            out.copy_(torch.from_numpy(np.ascontiguousarray(img)))
 
-        frame = tf.render(render_fn)
-        if rank == 0:
-            full, _, _ = orc.render(sc, sc.params(), threads=2)
-            q.put(bool(np.array_equal(frame.numpy(), full)))
+        tf = D.TiledFrames(sc.params(), band_rows=band_rows, groups_per_rank=groups, root=root)
+        got = {}
+        # two batches, the second starting mid-loop (its roots continue the rotation)
+        half = nframes // 2
+        got.update(tf.render(render_fn, half, 0))
+        got.update(tf.render(render_fn, nframes - half, half))
+        ok = True
+        for i, frame in got.items():
+            assert frame_root(i, world, root) == rank
+            s2 = S.Scene(sc.name, ubos[i], sc.tris, sc.models, sc.env, flags=sc.flags, max_depth=sc.max_depth)
+            full, _, _ = orc.render(s2, sc.params(), threads=2)
+            ok = ok and bool(np.array_equal(frame.numpy(), full))
+        q.put((rank, sorted(got), ok))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,band_rows,W,H", [(2, 8, 64, 50), (3, 4, 40, 33), (2, 64, 32, 20)])
-def test_tiled_frame_gloo(world, band_rows, W, H):
+@pytest.mark.parametrize("world,band_rows,groups,root,W,H", [
+    (2, 8, 1, ROOT_ROTATE, 64, 50),
+    (3, 4, 1, ROOT_ROTATE, 40, 33),
+    (3, 8, 2, 1, 48, 41),
+    (2, 64, 1, 0, 32, 20),
+])
+def test_tiled_frames_gloo(world, band_rows, groups, root, W, H):
+    nframes = 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, band_rows, W, H, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, band_rows, groups, root, nframes, W, H, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(120)
+        p.join(180)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert q.get(timeout=5) is True
+    res = [q.get(timeout=5) for _ in range(world)]
+    seen = sorted(i for _, frames, _ in res for i in frames)
+    assert seen == list(range(nframes))  # every frame assembled exactly once, on its root
+    assert all(ok for _, _, ok in res)
 
 
 @pytest.mark.parametrize("H,band_rows,world", [(768, 8, 8), (100, 8, 3), (7, 8, 4), (2160, 16, 8), (1, 1, 2)])
 def test_band_partition(H, band_rows, world):
-    """Every image row is rendered by exactly one rank; banded output rows match trt_output_rows."""
+    """Every image row is rendered by exactly one rank; banded output rows match trt_output_rows
+    and the C row mapping."""
     rows = [D.band_rows_of(H, band_rows, world, r) for r in range(world)]
     flat = sorted(sum(rows, []))
     assert flat == list(range(H))
@@ -73,6 +102,61 @@ def test_band_partition(H, band_rows, world):
     L = lib()
     for r in range(world):
         p = T.make_params(height=H, band_rows=band_rows, band_count=world, band_index=r)
-        import ctypes
-
         assert L.trt_output_rows(ctypes.byref(p)) == len(rows[r])
+        if world > 1:
+            assert [band_frame_row(k, band_rows, world, r) for k in range(len(rows[r]))] == rows[r]
+
+
+@pytest.mark.parametrize("W,H,B,N,G,F,root,self_gather", [
+    (1024, 768, 8, 8, 1, 16, ROOT_ROTATE, False),
+    (1024, 768, 8, 8, 1, 13, ROOT_ROTATE, True),
+    (3840, 2160, 8, 8, 1, 1, 0, False),
+    (236, 150, 16, 5, 3, 7, 2, False),
+    (64, 7, 8, 4, 2, 3, ROOT_ROTATE, False),
+    (1024, 768, 8, 1, 1, 4, ROOT_ROTATE, True),
+])
+def test_band_plan_invariants(W, H, B, N, G, F, root, self_gather):
+    """The plan delivers every row of every frame to the frame's root exactly once (the root's
+    own groups in place unless self_gather), within the buffers it sizes, without overlaps."""
+    lay, plan = band_plan(W, H, B, N, G, 0, F, root, self_gather)
+    NG = N * G
+    assert lay.groups == NG
+    assert lay.block_bytes == lay.max_rows * W * 4
+    assert lay.local_bytes == F * G * lay.block_bytes
+    rows_of = [len(T.output_rows(H, B, NG, g)) if NG > 1 else H for g in range(NG)]
+    assert lay.max_rows == max(rows_of)
+    delivered = {}
+    src_used, dst_used = {}, {}
+    for x in plan:
+        r = frame_root(x.frame, N, root)
+        assert x.dst == r and x.src == x.group // G
+        assert x.src != x.dst or self_gather
+        assert x.rows == rows_of[x.group] > 0 and x.bytes == x.rows * W * 4
+        assert x.src_offset == (x.frame * G + x.group % G) * lay.block_bytes
+        assert x.src_offset + x.bytes <= lay.local_bytes
+        assert x.dst_offset + x.bytes <= lay.gather_bytes
+        key = (x.frame, x.group)
+        assert key not in delivered
+        delivered[key] = x
+        for used, who, off in ((src_used, x.src, x.src_offset), (dst_used, x.dst, x.dst_offset)):
+            assert (who, off) not in used
+            used[(who, off)] = True
+    for f in range(F):
+        r = frame_root(f, N, root)
+        for g in range(NG):
+            own = g // G == r
+            if rows_of[g] == 0 or (own and not self_gather):
+                assert (f, g) not in delivered
+            else:
+                assert (f, g) in delivered
+    # with a rotating root every device roots ceil(F / N) frames at most
+    if root == ROOT_ROTATE:
+        assert lay.gather_bytes == -(-F // N) * NG * lay.block_bytes
+
+
+def test_band_plan_rejects_bad_shapes():
+    from vkcomputeshader_tinyraytracer_amd import TrtError
+
+    for args in ((0, 8, 8, 2, 1, 0, 1, 0), (8, 8, 0, 2, 1, 0, 1, 0), (8, 8, 8, 2, 1, 0, 1, 2), (8, 8, 8, 0, 1, 0, 1, 0)):
+        with pytest.raises(TrtError):
+            band_plan(*args)

@@ -4,9 +4,10 @@ bit-identical").
 * In one process: every rank's row bands (trt_params.band_*) rendered by the kernel and
   re-interleaved equal the whole-frame render bit for bit, for several world sizes, band
   heights and scenes (spheres-only and mesh/BVH).
-* Two processes on the one GPU of the box (gloo for the gather, since RCCL wants one device
-  per rank): TiledFrame + hip_render_fn give rank 0 exactly the single-process frame.  On an
-  8-GPU node the same code runs with backend "nccl" and one device per rank (bench.py)."""
+* Two and three processes on the one GPU of the box: dist.TiledFrames runs the native exchange
+  plan (trt_band_plan, the transfers trt_multi.cpp issues over RCCL) with gloo as transport
+  (RCCL wants one device per rank), the HIP kernel rendering each rank's band groups; every
+  frame lands on its rotating root equal to the single-process frame."""
 from __future__ import annotations
 
 import os
@@ -67,161 +68,48 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, W, H, band_rows, q):
+def _worker(rank, world, port, W, H, band_rows, groups, nframes, q):
     import torch
     import torch.distributed as dist
 
     import vkcomputeshader_tinyraytracer_amd as trt
+    from vkcomputeshader_tinyraytracer_amd.multi import ROOT_ROTATE
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sc = S.config_c2(W, H, env_size=ENV)
+        sc = S.config_c3(W, H, env_size=ENV)
+        ubos = np.stack([S.make_ubo(cam=(0.05 * i, 0.0, -0.1 * i)) for i in range(nframes)])
         r = trt.Renderer(0)
         r.upload_scene(sc)
-        tf = D.TiledFrame(W, H, band_rows=band_rows)  # gloo gathers host tensors
-        dev = torch.empty((tf.max_rows, W, 4), dtype=torch.uint8, device="cuda")
-        fn = D.hip_render_fn(r, sc.params(), band_rows, world, rank)
-
-        def render_fn(out):
-            fn(dev)
-            torch.cuda.synchronize()
-            out.copy_(dev.cpu())
-
-        frame = tf.render(render_fn)
-        if rank == 0:
+        tf = D.TiledFrames(sc.params(), band_rows=band_rows, groups_per_rank=groups, root=ROOT_ROTATE)
+        frames = tf.render(D.hip_render_fn(r, ubos), nframes)  # gloo moves host tensors
+        ok = True
+        for i, f in frames.items():
+            r.update_ubo(ubos[i])
             full, _, _ = r.draw_frame(sc.params())
-            q.put(bool(np.array_equal(frame.numpy(), full)))
+            ok = ok and bool(np.array_equal(f.numpy(), full))
+        q.put((rank, sorted(frames), ok))
         r.close()
     finally:
         dist.destroy_process_group()
 
 
-def test_tiled_frame_two_processes():
+@pytest.mark.parametrize("world,groups", [(2, 1), (3, 2)])
+def test_tiled_frames_processes(world, groups):
     import torch.multiprocessing as mp
 
-    W, H, world = 200, 120, 2
+    W, H, n = 200, 120, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, 8, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, 8, groups, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert q.get(timeout=5) is True
-
-
-def test_pipelined_tiles_frames_in_flight(gpu_renderer):
-    """dist.PipelinedTiles (the bench's tiled-frame leg): with two frames in flight every
-    submitted frame (distinct cameras) comes out equal to the one-at-a-time render."""
-    torch = pytest.importorskip("torch")
-    sc = S.config_c3(160, 96, env_size=ENV)
-    gpu_renderer.upload_scene(sc)
-    p = sc.params()
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    ubos = [S.make_ubo(cam=(0.05 * i, 0.0, -0.1 * i)) for i in range(5)]
-
-    def render(out, stream):
-        gpu_renderer.set_stream(stream)
-        gpu_renderer.draw_frame(p, out8=out)
-
-    try:
-        pipe = D.PipelinedTiles(p.width, p.height, 8, torch.device("cuda", 0), streams)
-        got = []
-        for u in ubos:
-            gpu_renderer.update_ubo(u)
-            img = pipe.submit(render)
-            pipe.comm.synchronize()
-            got.append(img.cpu().numpy().copy())
-    finally:
-        gpu_renderer.set_stream(None)
-    for u, g in zip(ubos, got):
-        gpu_renderer.update_ubo(u)
-        one, _, _ = gpu_renderer.draw_frame(p)
-        assert np.array_equal(g, one)
-    gpu_renderer.update_ubo(sc.ubo)
-
-
-def test_pipelined_tiles_deep_mesh_frame(gpu_renderer, golden_meshes):
-    """PipelinedTiles alternates trt_render between two streams; on a depth-20 mesh frame the
-    subtree split is active, so the two renders must not share task-queue scratch unfenced
-    (each stream gets its own split slot; a slot reused from another stream waits for it)."""
-    torch = pytest.importorskip("torch")
-    sc = S.config_reference_default(golden_meshes, env_size=ENV, width=160, height=120)
-    gpu_renderer.upload_scene(sc)
-    p = sc.params()
-    want, _, _ = gpu_renderer.draw_frame(p)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-
-    def render(out, stream):
-        gpu_renderer.set_stream(stream)
-        gpu_renderer.draw_frame(p, out8=out)
-
-    try:
-        pipe = D.PipelinedTiles(p.width, p.height, 8, torch.device("cuda", 0), streams)
-        got = []
-        for _ in range(6):
-            img = pipe.submit(render)
-            got.append(img)
-            if len(got) >= 2:  # the buffer of two submits ago is reused next: read it first
-                pipe.comm.synchronize()
-                got[-2] = got[-2].cpu().numpy().copy()
-        pipe.comm.synchronize()
-        got[-1] = got[-1].cpu().numpy().copy()
-    finally:
-        gpu_renderer.set_stream(None)
-    for g in got:
-        assert np.array_equal(g, want)
-
-
-def _nccl_worker(W, H, q):
-    import torch
-    import torch.distributed as dist
-
-    import vkcomputeshader_tinyraytracer_amd as trt
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(_free_port())
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        sc = S.config_c3(W, H, env_size=ENV)
-        r = trt.Renderer(0)
-        r.upload_scene(sc)
-        p = sc.params()
-        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-
-        def render(out, stream):
-            r.set_stream(stream)
-            r.draw_frame(p, out8=out)
-
-        pipe = D.PipelinedTiles(W, H, 8, torch.device("cuda", 0), streams)
-        assert pipe.tf[0].collective  # the gather runs through the process group
-        imgs = []
-        for _ in range(3):
-            img = pipe.submit(render)
-            pipe.comm.synchronize()
-            imgs.append(img.cpu().numpy().copy())
-        r.set_stream(None)
-        full, _, _ = r.draw_frame(p)
-        q.put(all(np.array_equal(i, full) for i in imgs))
-        r.close()
-    finally:
-        dist.destroy_process_group()
-
-
-def test_pipelined_tiles_nccl_world1():
-    """The RCCL ("nccl" backend) gather path of TiledFrame / PipelinedTiles executes at world
-    size 1 (the gather is not skipped when a process group exists)."""
-    import torch.multiprocessing as mp
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    pr = ctx.Process(target=_nccl_worker, args=(200, 120, q))
-    pr.start()
-    pr.join(240)
-    assert pr.exitcode == 0
-    assert q.get(timeout=5) is True
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert sorted(i for _, fr, _ in res for i in fr) == list(range(n))
+    assert all(ok for _, _, ok in res)

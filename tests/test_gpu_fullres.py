@@ -1,0 +1,39 @@
+"""Full-resolution parity of the larger configurations (BASELINE configs[2..4]) against the CPU
+oracle, on a spread of full-width rows.
+
+The reference renders one fixed 1024x768 frame (main.cpp:35-36, shader.comp:79-80); the
+build's larger configurations are checked elsewhere at reduced size.  Here the kernel renders
+a set of rows spread over the FULL frame — band_rows = 1, band_count = H / rows, band_index =
+i, i.e. rows i, i + band_count, ... — and the oracle (the shader.comp:338-399 restatement,
+linear batch loop) renders the same rows: 16 rows of C3 at 1920x1080, 16 rows of C4 at
+3840x2160, 4 rows of C5 at 3840x2160 and 16 spp.  Geometry counters must be equal, RGBA8
+within the parity bar (tests/helpers.py)."""
+from __future__ import annotations
+
+import pytest
+
+from oracle import oracle as orc
+from tests.helpers import assert_rgba8_close
+from vkcomputeshader_tinyraytracer_amd import scene as S, types as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("config,rows,index", [
+    ("C3", 16, 0), ("C3", 16, 37),
+    ("C4", 16, 0), ("C4", 16, 71),
+    ("C5", 4, 200),
+])
+def test_full_resolution_rows(gpu_renderer, config, rows, index):
+    sc = S.CONFIGS[config]()  # full size, reference envmap size
+    p = sc.params()
+    count = p.height // rows
+    p.band_rows, p.band_count, p.band_index = 1, count, index
+    gpu_renderer.upload_scene(sc)
+    g8, _, gst = gpu_renderer.draw_frame(p, count=True)
+    o8, _, ost = orc.render(sc, p, threads=0)
+    assert g8.shape == o8.shape == (len(T.output_rows(p.height, 1, count, index)), p.width, 4)
+    assert g8.shape[0] >= rows
+    for k in T.Stats.EXACT:
+        assert gst[k] == ost[k], (k, gst[k], ost[k])
+    assert_rgba8_close(g8, o8)

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as orc
-from tests.helpers import assert_float_close, assert_rgba8_close
+from tests.helpers import MAX_FRAC, assert_float_close, assert_rgba8_close
 from vkcomputeshader_tinyraytracer_amd import TrtError, scene as S, types as T
 
 pytestmark = pytest.mark.gpu
@@ -19,7 +19,7 @@ def _counts(st, keys=T.Stats.EXACT):
     return tuple(st[k] for k in keys)
 
 
-def _check(r, sc, params=None, want32=True, max_frac=0.02):
+def _check(r, sc, params=None, want32=True, max_frac=MAX_FRAC):
     """Kernel vs oracle; for mesh scenes both the per-ray BVH (default) and the
     reference-order batch walk (TRT_FLAG_BATCH_WALK) must match, the walk also in its
     batch/triangle work counters."""
@@ -257,22 +257,106 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
     out = torch.zeros((4, 64, 96, 4), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.Stream()
     gpu_renderer.set_stream(stream)
-    gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4, timing=True)
-    ms = gpu_renderer.frame_times(4)
-    torch.cuda.synchronize()
-    assert (ms > 0).all()
-    # sampled timing: frames 0 and 3 of 4 are bracketed; asking for more is an error
-    assert gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4,
-                                      timing=True, time_every=3) == 2
-    assert (gpu_renderer.frame_times(2) > 0).all()
-    with pytest.raises(TrtError):
-        gpu_renderer.frame_times(3)
-    torch.cuda.synchronize()
-    gpu_renderer.set_stream(None)
+    try:
+        # one launch per frame: every launch timed, per-frame times
+        gpu_renderer.set_frame_batch(1)
+        assert gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4, timing=True) == 4
+        ms = gpu_renderer.frame_times(4)
+        torch.cuda.synchronize()
+        assert (ms > 0).all()
+        assert list(gpu_renderer.launch_frames()) == [1, 1, 1, 1]
+        # sampled timing: launches 0 and 3 of 4 are bracketed; asking for more is an error
+        assert gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4,
+                                          timing=True, time_every=3) == 2
+        assert (gpu_renderer.frame_times(2) > 0).all()
+        with pytest.raises(TrtError):
+            gpu_renderer.frame_times(3)
+        # auto batching on one in-flight slot: the 4 camera-only frames are one launch; its
+        # time is per frame
+        gpu_renderer.set_frame_batch(0)
+        gpu_renderer.set_frames_in_flight(1)
+        assert gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4, timing=True) == 1
+        assert list(gpu_renderer.launch_frames()) == [4]
+        assert (gpu_renderer.frame_times(1) > 0).all()
+        # with 2 slots the frames are spread over two launches (one per hardware queue)
+        gpu_renderer.set_frames_in_flight(2)
+        assert gpu_renderer.render_frames(sc.params(), out, 4, ubos=ubos, frame_stride=64 * 96 * 4, timing=True) == 2
+        assert list(gpu_renderer.launch_frames()) == [2, 2]
+        torch.cuda.synchronize()
+    finally:
+        gpu_renderer.set_frame_batch(0)
+        gpu_renderer.set_frames_in_flight(0)
+        gpu_renderer.set_stream(None)
     for i in range(4):
         gpu_renderer.update_ubo(ubos[i])
         one, _, _ = gpu_renderer.draw_frame(sc.params())
         assert np.array_equal(out[i].cpu().numpy(), one)
+
+
+def _moving_ubos(n, sphere_every=0):
+    """Per-frame UBOs: the camera moves every frame (main.cpp:391-403); with sphere_every > 0
+    sphere 0 also moves every sphere_every frames, which splits a multi-frame launch there."""
+    ubos = []
+    for i in range(n):
+        u = S.make_ubo(cam=(0.07 * i, 0.02 * (i % 3), -0.1 * i))
+        if sphere_every and (i // sphere_every) % 2:
+            u["sphere0"]["center_radius"][0] += 0.25
+        ubos.append(u)
+    return np.stack(ubos)
+
+
+@pytest.mark.parametrize("batch,inflight", [(0, 0), (1, 0), (2, 1), (3, 2), (5, 3), (64, 1), (0, 4)])
+@pytest.mark.parametrize("config,sphere_every", [("C2", 0), ("C2", 4), ("C3", 3), ("C5", 0)])
+def test_multi_frame_launches_match_single_frames(gpu_renderer, config, sphere_every, batch, inflight):
+    """Multi-frame launches (trt_set_frame_batch): frame k of a launch owns blocks [k * ntiles,
+    (k + 1) * ntiles) with its own camera and image.  Every frame equals one-at-a-time trt_render
+    bit for bit, for launch sizes that divide the loop unevenly, UBOs that change more than the
+    camera (the launch splits there), a mesh scene (BVH walk) and 4 spp (the C5 sampler)."""
+    torch = pytest.importorskip("torch")
+    if config == "C5":
+        sc = S.CONFIGS["C3"](72, 40, env_size=SMALL_ENV)
+        p = sc.params(spp=4)
+    else:
+        sc = S.CONFIGS[config](88, 56, env_size=SMALL_ENV)
+        p = sc.params()
+    gpu_renderer.upload_scene(sc)
+    n = 11
+    ubos = _moving_ubos(n, sphere_every)
+    fb = p.height * p.width * 4
+    out = torch.zeros((n, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    gpu_renderer.set_stream(stream)
+    try:
+        gpu_renderer.set_frame_batch(batch)
+        gpu_renderer.set_frames_in_flight(inflight)
+        gpu_renderer.render_frames(p, out, n, ubos=ubos, frame_stride=fb, timing=True)
+        launches = gpu_renderer.launch_frames()
+        stream.synchronize()
+    finally:
+        gpu_renderer.set_frame_batch(0)
+        gpu_renderer.set_frames_in_flight(0)
+        gpu_renderer.set_stream(None)
+    assert int(launches.sum()) == n
+    # frames per launch: ceil(n / in-flight slots), at most the batch size (auto slots: 4)
+    per = max(1, min(batch or 64, -(-n // (inflight or 4))))
+    assert launches.max() <= per
+    if sphere_every:
+        assert len(launches) >= (n + sphere_every - 1) // sphere_every
+    else:
+        assert len(launches) == -(-n // per)
+    got = out.cpu().numpy()
+    for i in range(n):
+        gpu_renderer.update_ubo(ubos[i])
+        one, _, _ = gpu_renderer.draw_frame(p)
+        assert np.array_equal(got[i], one), i
+    gpu_renderer.update_ubo(sc.ubo)
+
+
+def test_frame_batch_bounds(gpu_renderer):
+    for bad in (65, 1000):
+        with pytest.raises(TrtError):
+            gpu_renderer.set_frame_batch(bad)
+    gpu_renderer.set_frame_batch(0)
 
 
 @pytest.mark.parametrize("inflight", [1, 2, 3, 4, 8, 0])

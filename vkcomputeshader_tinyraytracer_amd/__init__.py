@@ -9,6 +9,7 @@ from .scene import (
     MODEL_INFOS,
     Scene,
     SceneBuilder,
+    camera_path,
     config_c1,
     config_c2,
     config_c3,
@@ -23,6 +24,6 @@ from .scene import (
 
 __all__ = [
     "types", "ABI_SYMBOLS", "LIB_PATH", "TrtError", "lib", "Renderer", "render", "CONFIGS",
-    "MODEL_INFOS", "Scene", "SceneBuilder", "config_c1", "config_c2", "config_c3", "config_c4",
+    "MODEL_INFOS", "Scene", "SceneBuilder", "camera_path", "config_c1", "config_c2", "config_c3", "config_c4",
     "config_c5", "config_readme", "config_reference_default", "icosphere", "make_ubo", "synthetic_envmap", "write_image",
 ]

@@ -10,7 +10,7 @@ import ctypes
 import os
 from pathlib import Path
 
-from .types import Params, Stats
+from .types import BandLayout, BandXfer, Params, Stats
 
 _HERE = Path(__file__).resolve().parent
 # TRT_LIB may point at an experimental build of the same library (tools/build_variants.sh).
@@ -23,6 +23,19 @@ class TrtError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"trt error {code}: {msg}")
         self.code = code
+
+
+def raise_hw_queues() -> None:
+    """GPU_MAX_HW_QUEUES=32 when it is unset or at HIP's default (<= 4) and the operator did
+    not opt out (TRT_KEEP_HW_QUEUES=1).  Only effective before HIP initialises."""
+    if os.environ.get("TRT_KEEP_HW_QUEUES", "0") not in ("", "0"):
+        return
+    try:
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    except ValueError:
+        return
+    if cur <= 4:
+        os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 
 def lib() -> ctypes.CDLL:
@@ -40,9 +53,9 @@ def lib() -> ctypes.CDLL:
     # before torch is imported, torch's device init fails ("No HIP GPUs are available"); with
     # torch imported first both work.  So when torch is importable it is loaded first.
     # Frames in flight run on their own HIP streams: 32 hardware queues when the environment
-    # leaves HIP at its default of 4 (or less), set before torch or libtrt initialises HIP.
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) <= 4:
-        os.environ["GPU_MAX_HW_QUEUES"] = "32"
+    # leaves HIP at its default of 4 (or less), set once here, before torch or libtrt
+    # initialises HIP.  TRT_KEEP_HW_QUEUES=1 leaves an operator's setting alone.
+    raise_hw_queues()
     try:
         import torch  # noqa: F401
     except ImportError:
@@ -65,6 +78,8 @@ def lib() -> ctypes.CDLL:
         "trt_defer_stats": (c_int, [vp, c_u32, ctypes.POINTER(ctypes.c_uint64)]),
         "trt_render_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, vp, ctypes.c_size_t, c_u32]),
         "trt_frame_times": (c_int, [vp, ctypes.POINTER(ctypes.c_float), c_u32]),
+        "trt_timed_launches": (c_u32, [vp, ctypes.POINTER(c_u32), c_u32]),
+        "trt_set_frame_batch": (c_int, [vp, c_u32]),
         "trt_synchronize": (c_int, [vp]),
         "trt_output_rows": (c_u32, [ctypes.POINTER(Params)]),
         "trt_params_default": (None, [ctypes.POINTER(Params)]),
@@ -105,6 +120,12 @@ def lib() -> ctypes.CDLL:
         "trt_render_multi_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, c_u32, c_int, c_u32,
                                             ctypes.POINTER(vp), ctypes.c_size_t]),
         "trt_multi_synchronize": (c_int, [vp]),
+        "trt_multi_set_self_gather": (c_int, [vp, c_int]),
+        "trt_frame_root": (c_u32, [c_u32, c_u32, c_int]),
+        "trt_band_frame_row": (c_u32, [c_u32, c_u32, c_u32, c_u32]),
+        "trt_band_plan": (c_int, [c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_int, c_u32,
+                                  ctypes.POINTER(BandLayout), ctypes.POINTER(BandXfer), c_u32,
+                                  ctypes.POINTER(c_u32)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -130,6 +151,8 @@ ABI_SYMBOLS = (
     "trt_defer_stats",
     "trt_render_frames",
     "trt_frame_times",
+    "trt_timed_launches",
+    "trt_set_frame_batch",
     "trt_synchronize",
     "trt_output_rows",
     "trt_params_default",
@@ -168,4 +191,8 @@ ABI_SYMBOLS = (
     "trt_render_multi",
     "trt_render_multi_frames",
     "trt_multi_synchronize",
+    "trt_multi_set_self_gather",
+    "trt_frame_root",
+    "trt_band_frame_row",
+    "trt_band_plan",
 )

@@ -51,8 +51,10 @@ struct trt_ctx {
     uint32_t* d_persist = nullptr;
     uint32_t num_cus = 256;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::vector<hipEvent_t> fev; // per-frame event pairs of the last timed trt_render_frames
+    std::vector<hipEvent_t> fev; // per-launch event pairs of the last timed trt_render_frames
+    std::vector<uint32_t> fev_nframes; // frames traced by each timed launch
     uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
+    uint32_t frame_batch = TRT_FRAME_BATCH_AUTO; // frames per launch of a plain frame loop
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;
@@ -97,6 +99,20 @@ struct trt_ctx {
 constexpr size_t kPersistWords = 8 * 32; // 8 XCDs x (ticket, done) on their own 128-B lines
 
 namespace trt {
+
+// One frame of a frame loop: its UBO (null: the context's current one), its RGBA8 image (a
+// device pointer, or null) and whether a band launch writes its rows at their frame rows.
+struct FrameOut {
+    const trt_ubo* ubo;
+    uint8_t* out8;
+    bool in_place;
+};
+// The frame loop behind trt_render_frames and the multi-GPU band renders: plain frames go
+// out as multi-frame launches (up to kMaxLaunchFrames frames sharing everything but camPos and
+// the output), split / deferred-shadow frames one launch sequence per frame; launches rotate
+// over the frames-in-flight streams forked from and joined back into the context's stream.
+// Only enqueues.  time_every > 0: HIP events bracket every time_every-th launch.
+int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, uint32_t n, uint32_t time_every);
 
 // The scene bindings of a context in a fixed order (the RCCL scene broadcast walks them).
 enum SceneBuf : int {

@@ -153,6 +153,20 @@ struct SphereArg {
     Mat m;
 };
 
+// One frame of a launch.  A plain frame loop (trt_render_frames) traces up to
+// kMaxLaunchFrames frames per launch: block b renders tile b % ntiles of frame b / ntiles, so
+// one frame's slow tiles (the glass sphere) overlap the next frame's tiles inside one grid —
+// no stream switch, no launch gap, one drain per launch instead of per frame.  The frames of
+// a launch share every UBO field but the camera position (the reference's interactive loop
+// moves only camPos, main.cpp:391-403, 2165-2179) and each writes its own image.
+constexpr uint32_t kMaxLaunchFrames = 64;
+struct FrameRec {
+    float cam[3];      // UBO camPos (main.cpp:2170)
+    uint32_t in_place; // band launch: rows written at their frame rows (TRT_FLAG_BAND_IN_PLACE)
+    uint32_t* out8;    // packed RGBA8 of this frame (binding 3), or null
+};
+static_assert(sizeof(FrameRec) == 24, "FrameRec is 24 B");
+
 // Kernel arguments: the UBO (binding 0) travels in the kernarg segment, i.e. in SGPRs.
 struct KArgs {
     uint32_t width, height;
@@ -162,7 +176,7 @@ struct KArgs {
     uint32_t max_depth, spp, seed, flags;
     float dz;
     uint32_t nbatch;
-    float cam[3];
+    uint32_t nframes;   // frames of this launch (fr[0 .. nframes-1]), >= 1
     float light[3][3];
     SphereArg sph[4];
     const BatchRec* __restrict__ batches;
@@ -176,8 +190,7 @@ struct KArgs {
     const uint2* __restrict__ envp;
     uint32_t env_w, env_h;
     const float* __restrict__ rays_in; // Ray records (8 floats), or null
-    uint32_t* __restrict__ out8;       // packed RGBA8, or null
-    float* __restrict__ out32;         // float4 per pixel, or null
+    float* __restrict__ out32;         // float4 per pixel (rayOut, binding 2; single-frame launches), or null
     unsigned long long* __restrict__ counters; // trt_stats counters, in order (COUNT build)
     const BvhNode* __restrict__ bvh;  // per-lane BVH over triangles, or null (batch walk)
     const Bvh4Node* __restrict__ bvh4; // the same BVH collapsed to 4-wide nodes
@@ -218,6 +231,8 @@ struct KArgs {
     uint2* __restrict__ px_ev;        // per output pixel: (first chunk or kEvNone, events)
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
+    FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch
 };
+static_assert(sizeof(KArgs) <= 4096, "KArgs fits the 4 KB kernel-argument limit");
 
 } // namespace trt

@@ -22,8 +22,11 @@
 //     (-ffp-contract=off), IEEE-correct division and square root, NaN-ignoring min/max.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 
 #include "../../include/trt/abi.h"
+#include "trt_bands.h"
 #include "trt_device.h"
 #include "trt_math.h"
 
@@ -1434,8 +1437,7 @@ __device__ __forceinline__ f3 primary_dir(const KArgs& A, uint32_t x, uint32_t y
 
 __device__ __forceinline__ uint32_t band_row(const KArgs& A, uint32_t k) {
     if (A.band_rows == 0 || A.band_count <= 1) return k;
-    const uint32_t B = A.band_rows;
-    return ((k / B) * A.band_count + A.band_index) * B + (k % B);
+    return band_frame_row(k, A.band_rows, A.band_count, A.band_index); // trt_bands.h
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -1446,8 +1448,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 
 // Gamma (shader.comp:598) and the dual store (rayOut binding 2, storage image binding 3) of
 // output pixel o; `c` is the clamped colour.
-__device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
-    if (A.flags & TRT_FLAG_BAND_IN_PLACE) { // compact row k -> its frame row (band_row)
+__device__ __forceinline__ void store_pixel(const KArgs& A, const FrameRec& F, size_t o, f3 c) {
+    if (F.in_place) { // compact row k -> its frame row (band_row)
         const uint32_t k = (uint32_t)(o / A.width), x = (uint32_t)(o % A.width);
         o = (size_t)band_row(A, k) * A.width + x;
     }
@@ -1460,7 +1462,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
     {
         reinterpret_cast<float4*>(A.out32)[o] = make_float4(gx, gy, gz, 1.0f);
     }
-    if (A.out8) { // rgba8 storage image, shader.comp:61, 600
+    if (F.out8) { // rgba8 storage image, shader.comp:61, 600
         float ex = gx, ey = gy, ez = gz;
         if (A.flags & TRT_FLAG_SRGB_OUT) { // as displayed through the sRGB swapchain
             ex = srgb_encode(gx);
@@ -1470,7 +1472,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
         uint32_t r = (uint32_t)floorf(ex * 255.0f + 0.5f);
         uint32_t g = (uint32_t)floorf(ey * 255.0f + 0.5f);
         uint32_t b = (uint32_t)floorf(ez * 255.0f + 0.5f);
-        A.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
+        F.out8[o] = r | (g << 8) | (b << 16) | (255u << 24);
     }
 }
 
@@ -1478,18 +1480,19 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, size_t o, f3 c) {
 // (spp == 1 only): a pixel whose tree handed subtrees to the task queue parks its partial
 // colour in A.acc and is finished by finalize_spilled.
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
-__device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& cnt, float* lds, float4* slab) {
+__device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, uint32_t tile, Cnt& cnt, float* lds,
+                                           float4* slab) {
     const uint32_t lane = lane_id();
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;
 #ifdef TRT_DIAG_TRIVIAL
-    if (A.out8) A.out8[(size_t)k * A.width + x] = 0xff000000u | x; // diagnostic: launch + store only
+    if (F.out8) F.out8[(size_t)k * A.width + x] = 0xff000000u | x; // diagnostic: launch + store only
     return;
 #endif
     const uint32_t y = band_row(A, k);
-    const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
+    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
     const size_t o = (size_t)k * A.width + x;
     if (DEFER) { // pass A of a deferred-shadow frame (spp == 1)
         EvLog L;
@@ -1531,7 +1534,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
             base = __shfl(base, leader, 64);
             if (spilled) A.spilled[base + lane_rank(sp)] = (uint32_t)o;
         }
-        if (!spilled) store_pixel(A, o, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)));
+        if (!spilled) store_pixel(A, F, o, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)));
         return;
     }
     const uint32_t spp = A.spp ? A.spp : 1u;
@@ -1548,7 +1551,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, uint32_t tile, Cnt& c
     if (A.out32) reinterpret_cast<float4*>(A.out32)[o] = make_float4((float)cnt.wn, (float)cnt.wt, (float)cnt.wseg, (float)cnt.wmax);
     return;
 #endif
-    store_pixel(A, o, acc);
+    store_pixel(A, F, o, acc);
 }
 
 // Blocks b and b+8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md): give each XCD
@@ -1645,7 +1648,7 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
             j0 = __shfl(j0, 0, 64);
             if (j0 >= per) break;
             const uint32_t j1 = min(j0 + (uint32_t)TRT_PERSIST, per);
-            for (uint32_t j = j0; j < j1; ++j) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, xcd_tile(A, j * 8u + xc), cnt, lds, slab);
+            for (uint32_t j = j0; j < j1; ++j) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[0], xcd_tile(A, j * 8u + xc), cnt, lds, slab);
         }
         if (lane_id() == 0) {
             const uint32_t nw = (gridDim.x - xc + 7u) / 8u;
@@ -1659,10 +1662,17 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
     // diagnostic: TRT_TPW tiles per wave, grid-strided (b, b + G, ...; G % 8 == 0 keeps XCDs)
     for (uint32_t k = 0; k < TRT_TPW; ++k) {
         const uint32_t b = blockIdx.x + k * gridDim.x;
-        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, xcd_tile(A, b), cnt, lds, slab);
+        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[0], xcd_tile(A, b), cnt, lds, slab);
     }
 #else
-    trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, xcd_tile(A, vb), cnt, lds, slab);
+    // frame f = vb / ntiles of a multi-frame launch (plain frames only: split / deferred frames
+    // and counting passes launch one frame)
+    uint32_t f = 0, t = vb;
+    if (!SPLIT && !DEFER && A.nframes > 1u) {
+        f = vb / A.ntiles;
+        t = vb - f * A.ntiles;
+    }
+    trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], xcd_tile(A, t), cnt, lds, slab);
 #endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
@@ -1735,7 +1745,7 @@ __global__ __launch_bounds__(256) void finalize_spilled(KArgs A) {
         const uint32_t o = A.spilled[i];
         const unsigned long long* acc = A.acc + 4 * (size_t)o;
         const f3 c = mk(from_fixed(acc[0]), from_fixed(acc[1]), from_fixed(acc[2]));
-        store_pixel(A, o, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)));
+        store_pixel(A, A.fr[0], o, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z)));
     }
 }
 
@@ -1851,7 +1861,7 @@ __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
         }
         color = add(color, muls(add(muls(diffuse, p1.w), muls(specular, p2.w)), p3.x));
     }
-    store_pixel(A, o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
+    store_pixel(A, A.fr[0], o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
 }
 
 // Pixels whose log did not fit (event pool or query queue full) are traced again from scratch
@@ -1862,14 +1872,14 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KAr
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = A.dctr->nfb;
-    const f3 orig = mk(A.cam[0], A.cam[1], A.cam[2]);
+    const f3 orig = mk(A.fr[0].cam[0], A.fr[0].cam[1], A.fr[0].cam[2]);
     for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
         const uint32_t i = base + threadIdx.x;
         if (i < n) {
             const uint32_t o = A.fb[i];
             const uint32_t k = o / A.width, x = o % A.width;
             const f3 c = cast_ray<CAP, false, GEOM>(A, orig, primary_dir(A, x, band_row(A, k), 0), cnt, lds, slab);
-            store_pixel(A, o, c);
+            store_pixel(A, A.fr[0], o, c);
         }
     }
 }
@@ -2015,10 +2025,16 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
 #undef TRT_SPLIT_G
         return hipGetLastError();
     }
+    // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)
+#if !defined(TRT_PERSIST) && !defined(TRT_TPW) && TRT_WPB == 1
+    const dim3 fgrid(A.ntiles * std::max(A.nframes, 1u));
+#else
+    const dim3 fgrid = grid;
+#endif
 #define TRT_LAUNCH_G(CAP, G)                                                                             \
     do {                                                                                                 \
-        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G, false>), grid, block, 0, stream, A);   \
-        else hipLaunchKernelGGL((trace_kernel<CAP, false, G, false>), grid, block, 0, stream, A);        \
+        if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G, false>), fgrid, block, 0, stream, A);  \
+        else hipLaunchKernelGGL((trace_kernel<CAP, false, G, false>), fgrid, block, 0, stream, A);       \
     } while (0)
 #define TRT_LAUNCH(CAP)                          \
     do {                                         \
@@ -2075,7 +2091,8 @@ __global__ __launch_bounds__(256) void interleave_kernel(const uint32_t* __restr
                                                          uint32_t max_rows, size_t stride_px, int vec4,
                                                          uint32_t skip_lo, uint32_t skip_hi) {
     const uint32_t f = blockIdx.x / H, y = blockIdx.x % H;
-    const uint32_t b = y / B, g = b % NG, k = (b / NG) * B + y % B;
+    uint32_t g, k;
+    band_of_row(y, B, NG, g, k); // trt_bands.h
     if (g >= skip_lo && g < skip_hi) return; // the root's own groups, rendered in place
     const uint32_t* src = gather + ((size_t)(f * NG + g) * max_rows + k) * W;
     uint32_t* dst = out + (size_t)f * stride_px + (size_t)y * W;

@@ -1,12 +1,15 @@
-// trt_multi.cpp — one frame row-tiled over the GPUs of a node, gathered over RCCL (xGMI).
+// trt_multi.cpp — frames row-tiled over the GPUs of a node, gathered over RCCL (xGMI).
 //
 // The reference renders every frame on one GPU through one VkQueue (main.cpp:722-724,
-// dispatch main.cpp:2108-2131, submit main.cpp:2181-2205).  Here the frame's rows are dealt to
+// dispatch main.cpp:2108-2131, submit main.cpp:2181-2205).  Here a frame's rows are dealt to
 // the devices in interleaved bands (row y belongs to band group (y / B) % G_total, so the
-// costly image centre is spread over every device), each device renders its band groups with
-// the single-GPU kernel (trt_render with band_* params) into a compact RGBA8 buffer, and one
-// grouped ncclSend / ncclRecv moves the compact buffers to the frame's root device, where a
-// re-interleave kernel writes the frame.  The scene is uploaded once on rank 0 and broadcast
+// costly image centre is spread over every device: trt_bands.h), each device traces its band
+// groups of a batch of frames with the single-GPU kernel (multi-frame launches with band_*
+// params) into compact RGBA8 buffers, one grouped ncclSend / ncclRecv moves every frame's
+// compact buffers to that frame's root (the plan of band_plan.cpp: frame i's root is rank
+// i % N when the root rotates, so every device's links ingest at once), and a re-interleave
+// kernel writes the frames there.  The root traces its own bands straight into its frames
+// (in place), so they never travel.  The scene is uploaded once on rank 0 and broadcast
 // (ncclBroadcast of the packed device bindings), so a C++ host builds it only once.
 //
 // Two ways to create the communicator:
@@ -18,6 +21,11 @@
 // render stream per device, and the gathers run on a per-device communication stream, so a
 // batch's gather + re-interleave overlaps the next batch's render (the reference's
 // MAX_FRAMES_IN_FLIGHT = 2, main.cpp:45).
+//
+// Failure handling: every argument check and every allocation happens before a collective,
+// and allocations are agreed on by all ranks (a status all-reduce), so one rank's failure is
+// every rank's error instead of a hang.  An RCCL group is always closed (NcclGroup).  A failure
+// inside a collective section leaves the communicators aborted and the context unusable.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -28,6 +36,7 @@
 #include <vector>
 
 #include "../../include/trt/abi.h"
+#include "band_plan.h"
 #include "trt_ctx.h"
 
 namespace trt {
@@ -50,17 +59,21 @@ struct trt_multi {
         hipEvent_t fork = nullptr, join = nullptr;
         uint8_t* local[2] = {nullptr, nullptr}; // this device's compact band groups of a batch
         size_t local_cap[2] = {0, 0};
-        uint8_t* gather[2] = {nullptr, nullptr}; // all compact buffers of a batch (as root)
+        uint8_t* gather[2] = {nullptr, nullptr}; // the compact buffers of the frames it roots
         size_t gather_cap[2] = {0, 0};
         uint8_t* frame = nullptr; // trt_render_multi with host output: the root's frame
         size_t frame_cap = 0;
-        void* scratch = nullptr;  // scene header / counters
+        void* scratch = nullptr;  // scene header / counters / status words
     };
     std::vector<Dev> devs;
     uint32_t nranks = 1;
     uint32_t groups = 1; // band groups per rank
     uint64_t batch_seq = 0;
+    uint64_t frame_seq = 0; // frames of trt_render_multi (its rotating root)
     bool have_scene = false;
+    bool self_gather = false;
+    bool broken = false; // a collective failed midway: the communicators are aborted
+    int open_groups = 0; // RCCL groups opened by this context and not yet closed
     std::string err;
 };
 
@@ -74,6 +87,21 @@ int mfail(trt_multi* m, int code, const std::string& msg) {
     return code;
 }
 
+// A failure inside a collective section: other ranks may be blocked in the collective, so the
+// communicators are aborted (their pending operations fail instead of waiting forever) and the
+// context refuses further work.
+int poison(trt_multi* m, int code, const std::string& msg) {
+    // close the open group (if any) before the communicators it references go away
+    for (; m->open_groups > 0; --m->open_groups) (void)ncclGroupEnd();
+    for (auto& d : m->devs)
+        if (d.comm) {
+            (void)ncclCommAbort(d.comm);
+            d.comm = nullptr;
+        }
+    m->broken = true;
+    return mfail(m, code, msg + " (communicators aborted; destroy this context)");
+}
+
 #define MHIP(m, expr)                                                                            \
     do {                                                                                         \
         hipError_t e_ = (expr);                                                                  \
@@ -84,11 +112,47 @@ int mfail(trt_multi* m, int code, const std::string& msg) {
         ncclResult_t r_ = (expr);                                                                \
         if (r_ != ncclSuccess) return mfail((m), TRT_ERR_HIP, std::string(#expr ": ") + ncclGetErrorString(r_)); \
     } while (0)
+// inside a collective section (a group is open, or peers wait on this rank)
+#define CHIP(m, expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) return poison((m), TRT_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+#define CNCCL(m, expr)                                                                           \
+    do {                                                                                         \
+        ncclResult_t r_ = (expr);                                                                \
+        if (r_ != ncclSuccess) return poison((m), TRT_ERR_HIP, std::string(#expr ": ") + ncclGetErrorString(r_)); \
+    } while (0)
 #define MTRY(m, ctx, expr)                                                                       \
     do {                                                                                         \
         int rc_ = (expr);                                                                        \
         if (rc_ != TRT_OK) return mfail((m), rc_, std::string(#expr ": ") + trt_last_error(ctx)); \
     } while (0)
+
+// An RCCL group that is closed on every path out of its scope (poison() closes it first when
+// it aborts the communicators).
+struct NcclGroup {
+    trt_multi* m;
+    bool open = false;
+    explicit NcclGroup(trt_multi* mm) : m(mm) {}
+    ncclResult_t start() {
+        const ncclResult_t r = ncclGroupStart();
+        open = r == ncclSuccess;
+        if (open) ++m->open_groups;
+        return r;
+    }
+    ncclResult_t end() {
+        open = false;
+        --m->open_groups;
+        return ncclGroupEnd();
+    }
+    ~NcclGroup() {
+        if (open && m->open_groups > 0) {
+            --m->open_groups;
+            (void)ncclGroupEnd();
+        }
+    }
+};
 
 int init_dev(trt_multi* m, trt_multi::Dev& d) {
     int rc = trt_create(&d.ctx, d.device);
@@ -128,15 +192,52 @@ void free_dev(trt_multi::Dev& d) {
     if (d.ctx) trt_destroy(d.ctx);
 }
 
-int grow(trt_multi* m, int device, uint8_t** p, size_t* cap, size_t bytes) {
-    if (bytes <= *cap && *p) return TRT_OK;
-    MHIP(m, hipSetDevice(device));
-    MHIP(m, hipDeviceSynchronize()); // the old buffer may still be read by an in-flight batch
-    (void)hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    MHIP(m, hipMalloc(reinterpret_cast<void**>(p), bytes));
+// Grows *p to `bytes` (the device is synchronized first: an in-flight batch may read the old
+// buffer).  Returns false on failure (error text in m->err).
+bool grow(trt_multi* m, int device, uint8_t** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap && *p) return true;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) {
+        (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        e = hipMalloc(reinterpret_cast<void**>(p), bytes);
+    }
+    if (e != hipSuccess) {
+        m->err = std::string("multi-GPU buffer allocation: ") + hipGetErrorString(e);
+        return false;
+    }
     *cap = bytes;
+    return true;
+}
+
+// Sum over every device of every rank of `local` (one int per device of this process); the
+// collective that makes a local failure everybody's error.  Runs on the comm streams.
+int agree(trt_multi* m, const std::vector<int>& local, int& total) {
+    {
+        NcclGroup grp(m);
+        CNCCL(m, grp.start());
+        for (size_t i = 0; i < m->devs.size(); ++i) {
+            auto& d = m->devs[i];
+            CHIP(m, hipSetDevice(d.device));
+            int32_t* w = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d.scratch) + kScratchBytes - 64);
+            CHIP(m, hipMemcpyAsync(w, &local[i], sizeof(int32_t), hipMemcpyHostToDevice, d.comm_stream));
+            CNCCL(m, ncclAllReduce(w, w, 1, ncclInt32, ncclSum, d.comm, d.comm_stream));
+        }
+        CNCCL(m, grp.end());
+    }
+    total = 0;
+    auto& d0 = m->devs[0];
+    CHIP(m, hipSetDevice(d0.device));
+    int32_t v = 0;
+    CHIP(m, hipMemcpyAsync(&v, static_cast<uint8_t*>(d0.scratch) + kScratchBytes - 64, sizeof(v), hipMemcpyDeviceToHost,
+                           d0.comm_stream));
+    for (auto& d : m->devs) {
+        CHIP(m, hipSetDevice(d.device));
+        CHIP(m, hipStreamSynchronize(d.comm_stream));
+    }
+    total = v;
     return TRT_OK;
 }
 
@@ -144,6 +245,7 @@ int grow(trt_multi* m, int device, uint8_t** p, size_t* cap, size_t bytes) {
 trt_params group_params(const trt_params* p, uint32_t band_rows, uint32_t NG, uint32_t g) {
     trt_params q = *p;
     q.flags |= TRT_FLAG_DEVICE_PTRS;
+    q.flags &= ~TRT_FLAG_BAND_IN_PLACE;
     if (NG > 1) {
         q.band_rows = band_rows;
         q.band_count = NG;
@@ -156,124 +258,129 @@ trt_params group_params(const trt_params* p, uint32_t band_rows, uint32_t NG, ui
 
 int check_common(trt_multi* m, const trt_params* p, uint32_t band_rows, int root) {
     if (!m) return TRT_ERR_INVALID;
+    if (m->broken) return mfail(m, TRT_ERR_HIP, "multi context unusable after a failed collective: " + m->err);
     if (!p) return mfail(m, TRT_ERR_INVALID, "null params");
     if (!m->have_scene) return mfail(m, TRT_ERR_NOSCENE, "no scene uploaded (trt_multi_upload_scene)");
     if (band_rows == 0) return mfail(m, TRT_ERR_INVALID, "band_rows must be >= 1");
     if (p->band_rows && p->band_count > 1)
         return mfail(m, TRT_ERR_INVALID, "params must describe the whole frame (band_* = 0)");
     if (p->rays_in) return mfail(m, TRT_ERR_INVALID, "rays_in replay is a single-GPU (trt_render) feature");
+    if (p->width == 0 || p->height == 0) return mfail(m, TRT_ERR_INVALID, "empty frame");
     if (root != TRT_ROOT_ROTATE && (root < 0 || (uint32_t)root >= m->nranks))
         return mfail(m, TRT_ERR_INVALID, "root must be a rank or TRT_ROOT_ROTATE");
     return TRT_OK;
 }
 
-// One batch of `nf` frames: every local device renders its band groups of each frame into its
-// compact buffer (render stream of the slot), the compact buffers go to the batch's root over
-// RCCL (communication stream), and the root re-interleaves them into out + f * stride.
-int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t nf, uint32_t band_rows,
-              uint32_t root, bool rotate, uint8_t* const* out8, size_t frame_stride) {
-    const uint32_t N = m->nranks, G = m->groups, NG = N * G;
+// One batch of `nf` frames (frame f's root: trt_frame_root(rot0 + f, N, root)).  Every local
+// device traces its band groups of every frame (render stream of the slot) — a frame it roots
+// straight into out8[local] + f * frame_stride, the others compactly into its batch buffer —
+// the plan's transfers move the compact buffers to the roots over RCCL (communication stream),
+// and each root re-interleaves its frames.  out8[local] may be null: that device's frames are
+// not written.
+int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t nf, uint32_t band_rows, int root,
+              uint32_t rot0, uint8_t* const* out8, size_t frame_stride) {
+    const uint32_t N = m->nranks, G = m->groups;
     const uint32_t W = p->width, H = p->height;
-    uint32_t max_rows = 0;
-    std::vector<uint32_t> rows(NG);
-    for (uint32_t g = 0; g < NG; ++g) {
-        trt_params q = group_params(p, band_rows, NG, g);
-        rows[g] = trt_output_rows(&q);
-        max_rows = std::max(max_rows, rows[g]);
-    }
-    const size_t blk = (size_t)max_rows * W * 4; // one compact band-group buffer
+    trt_band_layout L{};
+    std::vector<trt_band_xfer> plan;
+    if (trt::build_band_plan(W, H, band_rows, N, G, rot0, nf, root, m->self_gather ? TRT_PLAN_SELF_GATHER : 0u, L,
+                             &plan) != TRT_OK)
+        return mfail(m, TRT_ERR_INVALID, "band plan: invalid batch");
+    const uint32_t NG = L.groups;
+    const size_t blk = L.block_bytes;
     const int slot = (int)(m->batch_seq & 1u);
     ++m->batch_seq;
-    // both slots grow together, and with a rotating root every device sizes its gather
-    // buffers, so no batch after the first one of a size allocates (grow synchronizes the
-    // device before it frees a buffer an in-flight batch may read)
-    for (auto& d : m->devs)
-        for (int s = 0; s < 2; ++s) {
-            if (grow(m, d.device, &d.local[s], &d.local_cap[s], blk * G * nf) != TRT_OK) return TRT_ERR_HIP;
-            if ((rotate || d.rank == root) && grow(m, d.device, &d.gather[s], &d.gather_cap[s], blk * NG * nf) != TRT_OK)
-                return TRT_ERR_HIP;
+    // Buffers: every device sizes its batch buffer and a gather buffer for a root of every frame
+    // (so the decision depends only on the batch shape, the same on every rank), both slots
+    // together; when anything grows the ranks agree on the outcome before the first collective.
+    const size_t need_local = L.local_bytes, need_gather = (size_t)nf * NG * blk;
+    bool grows = false;
+    for (auto& d : m->devs) grows = grows || need_local > d.local_cap[0] || need_gather > d.gather_cap[0];
+    if (grows) {
+        std::vector<int> bad(m->devs.size(), 0);
+        std::string why;
+        for (size_t i = 0; i < m->devs.size(); ++i) {
+            auto& d = m->devs[i];
+            for (int s = 0; s < 2 && !bad[i]; ++s)
+                if (!grow(m, d.device, &d.local[s], &d.local_cap[s], need_local) ||
+                    !grow(m, d.device, &d.gather[s], &d.gather_cap[s], need_gather)) {
+                    bad[i] = 1;
+                    why = m->err;
+                }
         }
+        int total = 0;
+        const int rc = agree(m, bad, total);
+        if (rc != TRT_OK) return rc;
+        if (total) return mfail(m, TRT_ERR_OOM, why.empty() ? "a peer rank failed to allocate its batch buffers" : why);
+    }
+    std::vector<uint32_t> froot(nf);
+    for (uint32_t f = 0; f < nf; ++f) froot[f] = trt_frame_root(rot0 + f, N, root);
     // render
-    size_t di = 0;
-    for (auto& d : m->devs) {
-        uint8_t* frame_out = (d.rank == root && out8) ? out8[di] : nullptr;
-        ++di;
+    std::vector<trt::FrameOut> fl(nf);
+    for (size_t li = 0; li < m->devs.size(); ++li) {
+        auto& d = m->devs[li];
         MHIP(m, hipSetDevice(d.device));
         hipStream_t rs = d.render[slot];
         if (d.gathered_valid[slot]) MHIP(m, hipStreamWaitEvent(rs, d.gathered[slot], 0));
         hipStream_t keep = d.ctx->stream;
         d.ctx->stream = rs;
-        // a band group's frames are 1/N of a frame each: the auto in-flight count of a tiled
-        // batch is 8 (C2 at 1 rank, 64 frames per gather: 24.4 -> 19.6 us per frame against 4,
-        // profiles/r02_multi_probe_inflight.log)
-        const uint32_t keep_fl = d.ctx->frames_in_flight;
-        if (!keep_fl) d.ctx->frames_in_flight = TRT_MAX_FRAMES_IN_FLIGHT;
-        // the batch's frames of each band group through the context's frame loop, so they run
-        // with its frames in flight (frame f's group v lands at local + (f * G + v) * blk)
         for (uint32_t v = 0; v < G; ++v) {
             const uint32_t g = d.rank * G + v;
-            if (!rows[g]) continue;
             trt_params q = group_params(p, band_rows, NG, g);
             q.flags &= ~(TRT_FLAG_COUNT | TRT_FLAG_TIMING);
-            q.flags |= TRT_FLAG_DEVICE_PTRS;
-            // the root's own groups: rendered in place into the output frames when there are
-            // any (no send, no re-interleave), else straight into the gather buffer
-            const bool own = d.rank == root;
-            uint8_t* dst = d.local[slot] + v * blk;
-            size_t stride = G * blk;
-            if (own && frame_out) {
-                q.flags |= TRT_FLAG_BAND_IN_PLACE;
-                dst = frame_out;
-                stride = frame_stride;
-            } else if (own) {
-                dst = d.gather[slot] + (size_t)g * blk;
-                stride = NG * blk;
+            if (!trt_output_rows(&q)) continue;
+            for (uint32_t f = 0; f < nf; ++f) {
+                const trt_ubo* u = ubos ? &ubos[f] : nullptr;
+                if (froot[f] == d.rank && !m->self_gather) // own frame: in place, never travels
+                    fl[f] = trt::FrameOut{u, (out8 && out8[li]) ? out8[li] + (size_t)f * frame_stride : nullptr, true};
+                else
+                    fl[f] = trt::FrameOut{u, d.local[slot] + ((size_t)f * G + v) * blk, false};
             }
-            const int rc = trt_render_frames(d.ctx, &q, ubos, nf, dst, stride, 0);
+            const int rc = trt::render_frame_list(d.ctx, &q, fl.data(), nf, 0);
             if (rc != TRT_OK) {
                 d.ctx->stream = keep;
-                d.ctx->frames_in_flight = keep_fl;
                 return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
             }
         }
-        if (ubos) d.ctx->ubo = ubos[nf - 1];
         d.ctx->stream = keep;
-        d.ctx->frames_in_flight = keep_fl;
         MHIP(m, hipEventRecord(d.rendered[slot], rs));
         MHIP(m, hipStreamWaitEvent(d.comm_stream, d.rendered[slot], 0));
     }
-    // gather: frame f, group g of rank r lands at gather + (f * NG + g) * blk on the root
-    MNCCL(m, ncclGroupStart());
-    for (auto& d : m->devs) {
-        MHIP(m, hipSetDevice(d.device));
-        for (uint32_t f = 0; f < nf; ++f) {
-            if (d.rank != root) {
-                for (uint32_t v = 0; v < G; ++v) {
-                    const uint32_t g = d.rank * G + v;
-                    if (rows[g])
-                        MNCCL(m, ncclSend(d.local[slot] + (f * G + v) * blk, (size_t)rows[g] * W * 4, ncclUint8,
-                                          (int)root, d.comm, d.comm_stream));
-                }
-                continue;
+    // gather: the plan's transfers, in list order on both ends (pairs match in order)
+    if (!plan.empty()) {
+        NcclGroup grp(m);
+        CNCCL(m, grp.start());
+        for (auto& d : m->devs) {
+            CHIP(m, hipSetDevice(d.device));
+            for (const trt_band_xfer& x : plan) {
+                if (x.src == d.rank)
+                    CNCCL(m, ncclSend(d.local[slot] + x.src_offset, x.bytes, ncclUint8, (int)x.dst, d.comm, d.comm_stream));
+                if (x.dst == d.rank)
+                    CNCCL(m, ncclRecv(d.gather[slot] + x.dst_offset, x.bytes, ncclUint8, (int)x.src, d.comm, d.comm_stream));
             }
-            for (uint32_t g = 0; g < NG; ++g)
-                if (rows[g] && g / G != root)
-                    MNCCL(m, ncclRecv(d.gather[slot] + (f * NG + g) * blk, (size_t)rows[g] * W * 4, ncclUint8,
-                                      (int)(g / G), d.comm, d.comm_stream));
         }
+        CNCCL(m, grp.end());
     }
-    MNCCL(m, ncclGroupEnd());
-    size_t li = 0;
-    for (auto& d : m->devs) {
+    // re-interleave: a root's frames of the batch are f0, f0 + step, ... (rotation) or all
+    for (size_t li = 0; li < m->devs.size(); ++li) {
+        auto& d = m->devs[li];
         MHIP(m, hipSetDevice(d.device));
-        if (d.rank == root && out8 && out8[li]) {
+        uint32_t f0 = nf, cnt = 0;
+        for (uint32_t f = 0; f < nf; ++f)
+            if (froot[f] == d.rank) {
+                if (f0 == nf) f0 = f;
+                ++cnt;
+            }
+        if (cnt && out8 && out8[li]) {
+            const uint32_t step = root == TRT_ROOT_ROTATE ? N : 1u;
+            const uint32_t lo = m->self_gather ? 0u : d.rank * G, hi = m->self_gather ? 0u : d.rank * G + G;
             MHIP(m, trt::launch_interleave(reinterpret_cast<const uint32_t*>(d.gather[slot]),
-                                           reinterpret_cast<uint32_t*>(out8[li]), W, H, band_rows, NG, max_rows, nf,
-                                           frame_stride / 4, d.comm_stream, root * G, root * G + G));
+                                           reinterpret_cast<uint32_t*>(out8[li] + (size_t)f0 * frame_stride), W, H,
+                                           band_rows, NG, L.max_rows, cnt, (size_t)step * frame_stride / 4,
+                                           d.comm_stream, lo, hi));
         }
         MHIP(m, hipEventRecord(d.gathered[slot], d.comm_stream));
         d.gathered_valid[slot] = true;
-        ++li;
     }
     return TRT_OK;
 }
@@ -388,47 +495,77 @@ int trt_multi_set_band_groups(trt_multi* m, uint32_t groups_per_rank) {
     return TRT_OK;
 }
 
+int trt_multi_set_self_gather(trt_multi* m, int on) {
+    if (!m) return TRT_ERR_INVALID;
+    m->self_gather = on != 0;
+    return TRT_OK;
+}
+
 int trt_multi_upload_scene(trt_multi* m, const trt_ubo* ubo, const trt_triangle* tris, uint32_t ntri,
                            const trt_model* models, uint32_t nmodel, const uint8_t* env, uint32_t env_w,
                            uint32_t env_h) {
     if (!m) return TRT_ERR_INVALID;
+    if (m->broken) return mfail(m, TRT_ERR_HIP, "multi context unusable after a failed collective: " + m->err);
     m->have_scene = false;
-    // 1. rank 0 builds the device bindings from the AoS records (BVH, SoA repack, envmap)
+    // 1. rank 0 builds the device bindings from the AoS records (BVH, SoA repack, envmap); a
+    //    failure there travels as a header with magic 0, so every rank returns an error
+    int rc0 = TRT_OK;
+    std::string why;
     for (auto& d : m->devs) {
         if (d.rank != 0) continue;
-        MTRY(m, d.ctx, trt_upload_scene(d.ctx, ubo, tris, ntri, models, nmodel, env, env_w, env_h));
-        trt::SceneHeader h;
-        trt::scene_header(d.ctx, h);
+        trt::SceneHeader h{};
+        rc0 = trt_upload_scene(d.ctx, ubo, tris, ntri, models, nmodel, env, env_w, env_h);
+        if (rc0 == TRT_OK) trt::scene_header(d.ctx, h);
+        else why = std::string("trt_upload_scene on rank 0: ") + trt_last_error(d.ctx);
         MHIP(m, hipSetDevice(d.device));
         MHIP(m, hipMemcpy(d.scratch, &h, sizeof(h), hipMemcpyHostToDevice));
     }
-    // 2. the header, then every binding, broadcast from rank 0 (ncclBroadcast over xGMI)
-    MNCCL(m, ncclGroupStart());
-    for (auto& d : m->devs) {
-        MHIP(m, hipSetDevice(d.device));
-        MNCCL(m, ncclBroadcast(d.scratch, d.scratch, sizeof(trt::SceneHeader), ncclUint8, 0, d.comm, d.comm_stream));
-    }
-    MNCCL(m, ncclGroupEnd());
-    trt::SceneHeader h{};
-    for (auto& d : m->devs) {
-        MHIP(m, hipSetDevice(d.device));
-        MHIP(m, hipStreamSynchronize(d.comm_stream));
-        MHIP(m, hipMemcpy(&h, d.scratch, sizeof(h), hipMemcpyDeviceToHost));
-        if (d.rank != 0) MTRY(m, d.ctx, trt::scene_adopt(d.ctx, h));
-    }
-    MNCCL(m, ncclGroupStart());
-    for (int k = 0; k < trt::kSceneBufs; ++k) {
-        if (!h.bytes[k]) continue;
+    // 2. the header broadcast from rank 0 (ncclBroadcast over xGMI)
+    {
+        NcclGroup grp(m);
+        CNCCL(m, grp.start());
         for (auto& d : m->devs) {
-            MHIP(m, hipSetDevice(d.device));
-            void* p = *trt::scene_buf(d.ctx, k);
-            MNCCL(m, ncclBroadcast(p, p, h.bytes[k], ncclUint8, 0, d.comm, d.comm_stream));
+            CHIP(m, hipSetDevice(d.device));
+            CNCCL(m, ncclBroadcast(d.scratch, d.scratch, sizeof(trt::SceneHeader), ncclUint8, 0, d.comm, d.comm_stream));
+        }
+        CNCCL(m, grp.end());
+    }
+    trt::SceneHeader h{};
+    std::vector<int> bad(m->devs.size(), 0);
+    for (size_t i = 0; i < m->devs.size(); ++i) {
+        auto& d = m->devs[i];
+        CHIP(m, hipSetDevice(d.device));
+        CHIP(m, hipStreamSynchronize(d.comm_stream));
+        CHIP(m, hipMemcpy(&h, d.scratch, sizeof(h), hipMemcpyDeviceToHost));
+        if (h.magic != trt::kSceneMagic) return mfail(m, rc0 != TRT_OK ? rc0 : TRT_ERR_INVALID,
+                                                      why.empty() ? "rank 0 failed to build the scene" : why);
+        if (d.rank != 0 && trt::scene_adopt(d.ctx, h) != TRT_OK) {
+            bad[i] = 1;
+            why = std::string("scene adoption: ") + trt_last_error(d.ctx);
         }
     }
-    MNCCL(m, ncclGroupEnd());
+    // 3. every rank agrees that every device holds buffers for the bindings
+    int total = 0;
+    const int rc = agree(m, bad, total);
+    if (rc != TRT_OK) return rc;
+    if (total) return mfail(m, TRT_ERR_OOM, why.empty() ? "a peer rank failed to allocate the scene" : why);
+    // 4. every binding broadcast from rank 0
+    {
+        NcclGroup grp(m);
+        CNCCL(m, grp.start());
+        for (int k = 0; k < trt::kSceneBufs; ++k) {
+            if (!h.bytes[k]) continue;
+            for (auto& d : m->devs) {
+                CHIP(m, hipSetDevice(d.device));
+                void* p = *trt::scene_buf(d.ctx, k);
+                CNCCL(m, ncclBroadcast(p, p, h.bytes[k], ncclUint8, 0, d.comm, d.comm_stream));
+            }
+        }
+        CNCCL(m, grp.end());
+    }
     for (auto& d : m->devs) {
-        MHIP(m, hipSetDevice(d.device));
-        MHIP(m, hipStreamSynchronize(d.comm_stream));
+        CHIP(m, hipSetDevice(d.device));
+        CHIP(m, hipStreamSynchronize(d.comm_stream));
     }
     m->have_scene = true;
     return TRT_OK;
@@ -444,34 +581,32 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
                      trt_stats* st) {
     int rc = check_common(m, p, band_rows, root);
     if (rc != TRT_OK) return rc;
-    if (root == TRT_ROOT_ROTATE) root = (int)(m->batch_seq % m->nranks);
+    const uint32_t r = trt_frame_root((uint32_t)(m->frame_seq++ % m->nranks), m->nranks, root);
     const bool dev_out = (p->flags & TRT_FLAG_DEVICE_PTRS) != 0;
     const size_t frame_bytes = (size_t)p->width * p->height * 4;
     // host output: the root renders into its own device frame and copies it out
     std::vector<uint8_t*> outs(m->devs.size(), nullptr);
-    size_t li = 0;
-    for (auto& d : m->devs) {
-        if ((int)d.rank == root && out8 && out8[li]) {
+    for (size_t li = 0; li < m->devs.size(); ++li) {
+        auto& d = m->devs[li];
+        if (d.rank == r && out8 && out8[li]) {
             if (dev_out) {
                 outs[li] = out8[li];
             } else {
-                if (grow(m, d.device, &d.frame, &d.frame_cap, frame_bytes) != TRT_OK) return TRT_ERR_HIP;
+                if (!grow(m, d.device, &d.frame, &d.frame_cap, frame_bytes)) return TRT_ERR_OOM;
                 outs[li] = d.frame;
             }
         }
-        ++li;
     }
     if ((rc = fork_all(m)) != TRT_OK) return rc;
-    if ((rc = run_batch(m, p, nullptr, 1, band_rows, (uint32_t)root, false, outs.data(), 0)) != TRT_OK) return rc;
+    if ((rc = run_batch(m, p, nullptr, 1, band_rows, (int)r, 0, outs.data(), 0)) != TRT_OK) return rc;
     if ((rc = join_all(m)) != TRT_OK) return rc;
-    li = 0;
-    for (auto& d : m->devs) {
+    for (size_t li = 0; li < m->devs.size(); ++li) {
+        auto& d = m->devs[li];
         if (!dev_out && outs[li]) {
             MHIP(m, hipSetDevice(d.device));
             MHIP(m, hipMemcpyAsync(out8[li], outs[li], frame_bytes, hipMemcpyDeviceToHost, d.ctx->stream));
             MHIP(m, hipStreamSynchronize(d.ctx->stream));
         }
-        ++li;
     }
     if (st) {
         // Counters: a separate counting pass of every band group (trt_render COUNT), summed over
@@ -479,13 +614,19 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
         std::memset(st, 0, sizeof(*st));
         if (p->flags & TRT_FLAG_COUNT) {
             const uint32_t NG = m->nranks * m->groups;
+            // word 20: local failures (a failed counting pass still joins the all-reduce)
+            std::string why;
             for (auto& d : m->devs) {
-                uint64_t sum[20] = {0};
-                for (uint32_t v = 0; v < m->groups; ++v) {
+                uint64_t sum[21] = {0};
+                for (uint32_t v = 0; v < m->groups && !sum[20]; ++v) {
                     trt_params q = group_params(p, band_rows, NG, d.rank * m->groups + v);
                     q.flags &= ~(TRT_FLAG_DEVICE_PTRS | TRT_FLAG_TIMING);
                     trt_stats s{};
-                    MTRY(m, d.ctx, trt_render(d.ctx, &q, nullptr, nullptr, &s));
+                    if (trt_render(d.ctx, &q, nullptr, nullptr, &s) != TRT_OK) {
+                        sum[20] = 1;
+                        why = std::string("counting pass: ") + trt_last_error(d.ctx);
+                        break;
+                    }
                     const uint64_t vk[20] = {s.primary_rays, s.secondary_rays, s.shadow_rays, s.misses, s.tri_nearest,
                                              s.sphere_tests, s.batch_tests, s.batch_hits, s.tri_tests, s.node_tests,
                                              s.tri_past_a, s.tri_past_u, s.tri_past_v, s.shadow_skipped,
@@ -493,24 +634,28 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
                                              s.skipped_tri_past_a, s.skipped_tri_past_u, s.skipped_tri_past_v};
                     for (int k = 0; k < 20; ++k) sum[k] += vk[k];
                 }
-                MHIP(m, hipSetDevice(d.device));
-                MHIP(m, hipMemcpy(d.scratch, sum, sizeof(sum), hipMemcpyHostToDevice));
+                CHIP(m, hipSetDevice(d.device));
+                CHIP(m, hipMemcpy(d.scratch, sum, sizeof(sum), hipMemcpyHostToDevice));
             }
-            MNCCL(m, ncclGroupStart());
-            for (auto& d : m->devs) {
-                MHIP(m, hipSetDevice(d.device));
-                MNCCL(m, ncclAllReduce(d.scratch, d.scratch, 20, ncclUint64, ncclSum, d.comm, d.comm_stream));
+            {
+                NcclGroup grp(m);
+                CNCCL(m, grp.start());
+                for (auto& d : m->devs) {
+                    CHIP(m, hipSetDevice(d.device));
+                    CNCCL(m, ncclAllReduce(d.scratch, d.scratch, 21, ncclUint64, ncclSum, d.comm, d.comm_stream));
+                }
+                CNCCL(m, grp.end());
             }
-            MNCCL(m, ncclGroupEnd());
-            uint64_t tot[20] = {0};
+            uint64_t tot[21] = {0};
             auto& d0 = m->devs[0];
-            MHIP(m, hipSetDevice(d0.device));
-            MHIP(m, hipStreamSynchronize(d0.comm_stream));
-            MHIP(m, hipMemcpy(tot, d0.scratch, sizeof(tot), hipMemcpyDeviceToHost));
+            CHIP(m, hipSetDevice(d0.device));
+            CHIP(m, hipStreamSynchronize(d0.comm_stream));
+            CHIP(m, hipMemcpy(tot, d0.scratch, sizeof(tot), hipMemcpyDeviceToHost));
             for (auto& d : m->devs) {
-                MHIP(m, hipSetDevice(d.device));
-                MHIP(m, hipStreamSynchronize(d.comm_stream));
+                CHIP(m, hipSetDevice(d.device));
+                CHIP(m, hipStreamSynchronize(d.comm_stream));
             }
+            if (tot[20]) return mfail(m, TRT_ERR_HIP, why.empty() ? "a peer rank's counting pass failed" : why);
             st->primary_rays = tot[0];
             st->secondary_rays = tot[1];
             st->shadow_rays = tot[2];
@@ -546,16 +691,15 @@ int trt_render_multi_frames(trt_multi* m, const trt_params* p, const trt_ubo* ub
     if (p->flags & (TRT_FLAG_COUNT | TRT_FLAG_TIMING))
         return mfail(m, TRT_ERR_INVALID, "trt_render_multi_frames: COUNT/TIMING are trt_render_multi flags");
     if (frame_stride % 4) return mfail(m, TRT_ERR_INVALID, "frame_stride must be a multiple of 4");
-    const uint32_t F = std::max(frames_per_gather, 1u);
+    const uint32_t F = std::min(std::max(frames_per_gather, 1u), TRT_MAX_FRAME_BATCH);
     if ((rc = fork_all(m)) != TRT_OK) return rc;
     std::vector<uint8_t*> outs(m->devs.size());
     for (uint32_t i0 = 0; i0 < nframes; i0 += F) {
         const uint32_t nf = std::min(F, nframes - i0);
-        const uint32_t r = root == TRT_ROOT_ROTATE ? (uint32_t)(m->batch_seq % m->nranks) : (uint32_t)root;
         for (size_t li = 0; li < m->devs.size(); ++li)
             outs[li] = (out8 && out8[li]) ? out8[li] + (size_t)i0 * frame_stride : nullptr;
-        if ((rc = run_batch(m, p, ubos ? ubos + i0 : nullptr, nf, band_rows, r, root == TRT_ROOT_ROTATE, outs.data(),
-                            frame_stride)) != TRT_OK)
+        if ((rc = run_batch(m, p, ubos ? ubos + i0 : nullptr, nf, band_rows, root, i0, outs.data(), frame_stride)) !=
+            TRT_OK)
             return rc;
     }
     return join_all(m);

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <limits>
 #include <cstring>
@@ -21,6 +22,7 @@
 
 #include "../../include/trt/abi.h"
 #include "jpeg.h"
+#include "trt_bands.h"
 #include "trt_ctx.h"
 #include "trt_device.h"
 
@@ -127,14 +129,23 @@ void fill_ubo_args(KArgs& A, const trt_ubo& u) {
         A.light[i][1] = l[i]->y;
         A.light[i][2] = l[i]->z;
     }
-    A.cam[0] = u.camPos.x;
-    A.cam[1] = u.camPos.y;
-    A.cam[2] = u.camPos.z;
 }
 
-bool row_selected(const trt_params* p, uint32_t r) {
-    if (p->band_rows == 0 || p->band_count <= 1) return true;
-    return (r / p->band_rows) % p->band_count == p->band_index;
+void fill_frame(trt::FrameRec& f, const trt_ubo& u, uint8_t* out8, bool in_place) {
+    f.cam[0] = u.camPos.x;
+    f.cam[1] = u.camPos.y;
+    f.cam[2] = u.camPos.z;
+    f.in_place = in_place ? 1u : 0u;
+    f.out8 = reinterpret_cast<uint32_t*>(out8);
+}
+
+// Frames that may share a launch: every UBO field but camPos equal (byte-wise).
+bool same_but_camera(const trt_ubo& a, const trt_ubo& b) {
+    constexpr size_t cam = offsetof(trt_ubo, camPos);
+    return std::memcmp(&a, &b, cam) == 0 &&
+           std::memcmp(reinterpret_cast<const char*>(&a) + cam + sizeof(trt_vec4),
+                       reinterpret_cast<const char*>(&b) + cam + sizeof(trt_vec4),
+                       sizeof(trt_ubo) - cam - sizeof(trt_vec4)) == 0;
 }
 
 } // namespace
@@ -157,9 +168,8 @@ void trt_params_default(trt_params* p) {
 uint32_t trt_output_rows(const trt_params* p) {
     if (!p) return 0;
     if (p->band_rows == 0 || p->band_count <= 1) return p->height;
-    uint32_t n = 0;
-    for (uint32_t r = 0; r < p->height; ++r) n += row_selected(p, r) ? 1u : 0u;
-    return n;
+    if (p->band_index >= p->band_count) return 0;
+    return trt::band_group_rows(p->height, p->band_rows, p->band_count, p->band_index);
 }
 
 int trt_create(trt_ctx** out, int hip_device) {
@@ -167,12 +177,6 @@ int trt_create(trt_ctx** out, int hip_device) {
     *out = nullptr;
     trt_ctx* c = new (std::nothrow) trt_ctx();
     if (!c) return TRT_ERR_OOM;
-    // frames in flight are HIP streams: ask for 32 hardware queues when the environment leaves
-    // HIP at its default of 4 (or less); no effect once HIP is initialised in this process
-    {
-        const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-        if (!q || std::atoi(q) <= 4) setenv("GPU_MAX_HW_QUEUES", "32", 1);
-    }
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0 || hip_device < 0 || hip_device >= n) {
@@ -563,6 +567,8 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.dz = (float)(-1.0 * ((double)p->height / (2.0 * std::tan((double)p->fov / 2.0))));
     A.nbatch = c->nbatch;
     fill_ubo_args(A, c->ubo);
+    A.nframes = 1;
+    fill_frame(A.fr[0], c->ubo, nullptr, (p->flags & TRT_FLAG_BAND_IN_PLACE) != 0);
     A.batches = c->d_batches;
     A.geo = c->d_geo;
     A.shade = c->d_shade;
@@ -771,8 +777,10 @@ uint32_t render_slot(trt_ctx* c, hipStream_t s) {
 
 } // namespace
 
-extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
-                                 uint8_t* out8, size_t frame_stride, uint32_t time_every) {
+namespace trt {
+
+int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, uint32_t nframes,
+                      uint32_t time_every) {
     if (!c) return TRT_ERR_INVALID;
     int rc = check_params(c, p);
     if (rc != TRT_OK) return rc;
@@ -780,30 +788,53 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
         return fail(c, TRT_ERR_INVALID, "trt_render_frames: needs TRT_FLAG_DEVICE_PTRS");
     if (p->flags & TRT_FLAG_COUNT)
         return fail(c, TRT_ERR_INVALID, "trt_render_frames: COUNT is a per-frame trt_render flag");
+    if (nframes && !frames) return fail(c, TRT_ERR_INVALID, "trt_render_frames: null frame list");
     HIP_TRY(c, hipSetDevice(c->device));
-    const bool timing = (p->flags & TRT_FLAG_TIMING) != 0;
-    const uint32_t every = time_every ? time_every : 1u;
+    const bool timing = time_every > 0;
+    const uint32_t every = timing ? time_every : 1u;
     c->fev_frames = 0;
+    c->fev_nframes.clear();
+    if ((rc = ensure_envp(c, p, c->stream)) != TRT_OK) return rc;
+    KArgs A;
+    fill_args(c, p, A);
+    A.rays_in = reinterpret_cast<const float*>(p->rays_in);
+    auto ubo_of = [&](uint32_t i) -> const trt_ubo& { return frames[i].ubo ? *frames[i].ubo : c->ubo; };
+    if (A.rows == 0 || nframes == 0) {
+        if (nframes) c->ubo = ubo_of(nframes - 1);
+        return TRT_OK;
+    }
+    // Plain frames (no subtree split, no deferred shadows: the same decision prepare_split
+    // makes) go out several per launch; the others one per launch (per-slot scratch).
+    const bool defer = defer_frame(c, p);
+    const bool split = (defer || !defer_frame(c, p, true)) && split_window(c, p) != 0;
+    const bool plain = !defer && !split;
+    // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): launch j runs on slot j % n.  Slot 0
+    // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
+    // joined back into it below, so to the caller all frames complete on its stream.  Auto: 4
+    // (C2 -13 % at 4 vs 2, profiles/r02_ab_queues_c2.log), or 8 for deferred-shadow frames (the
+    // shipped frame 1.45 -> 0.56 ms at 8, r02_ab_queues_deep.log).  Each slot is a hardware
+    // queue with its own dispatcher: a C2 frame's 12,288 one-wave workgroups are
+    // dispatch-limited on one queue (16.5 us per frame inside one multi-frame launch against
+    // 13.8 us with 4 queues feeding the GPU), so a plain loop spreads its multi-frame launches
+    // over the slots: ceil(nframes / slots) frames per launch, at most frame_batch.
+    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : defer ? 8u : 4u;
+    const uint32_t cap = plain ? (c->frame_batch ? c->frame_batch : trt::kMaxLaunchFrames) : 1u;
+    const uint32_t per_launch = std::max(1u, std::min(cap, (nframes + want - 1) / want));
+    // launches: runs of consecutive frames sharing every UBO field but camPos
+    std::vector<uint32_t> first{0};
+    for (uint32_t i = 1; i < nframes; ++i)
+        if (i - first.back() >= per_launch || !same_but_camera(ubo_of(i), ubo_of(first.back()))) first.push_back(i);
+    const uint32_t nl = (uint32_t)first.size();
+    first.push_back(nframes);
     if (timing) {
-        const uint32_t ntimed = (nframes + every - 1) / every; // frames 0, every, 2*every, ...
+        const uint32_t ntimed = (nl + every - 1) / every; // launches 0, every, 2*every, ...
         while (c->fev.size() < 2 * (size_t)ntimed) {
             hipEvent_t e;
             HIP_TRY(c, hipEventCreate(&e));
             c->fev.push_back(e);
         }
     }
-    if ((rc = ensure_envp(c, p, c->stream)) != TRT_OK) return rc;
-    KArgs A;
-    fill_args(c, p, A);
-    A.rays_in = reinterpret_cast<const float*>(p->rays_in);
-    if (A.rows == 0) return TRT_OK;
-    // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): frame i runs on slot i % n.  Slot 0
-    // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
-    // joined back into it below, so to the caller all frames complete on its stream.
-    // auto: 4, or 8 for deferred-shadow frames (C2 -13 % at 4 vs 2; the shipped frame 1.45 ->
-    // 0.56 ms at 8: profiles/r02_ab_queues_c2.log, r02_ab_queues_deep.log)
-    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : (defer_frame(c, p) ? 8u : 4u);
-    const uint32_t nfl = std::min(want, std::max(nframes, 1u));
+    const uint32_t nfl = std::min(want, nl);
     std::vector<hipStream_t> sv{c->stream};
     if (nfl > 1) {
         while (c->aux.size() < nfl - 1) {
@@ -821,24 +852,27 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
             sv.push_back(c->aux[k]);
         }
     }
-    for (uint32_t i = 0; i < nframes; ++i) {
-        if (ubos) {
-            c->ubo = ubos[i];
-            fill_ubo_args(A, c->ubo);
-        }
-        hipStream_t st = sv[i % nfl];
-        if ((rc = prepare_split(c, p, A, i % nfl, st)) != TRT_OK) return rc;
-        A.out8 = out8 ? reinterpret_cast<uint32_t*>(out8 + (size_t)i * frame_stride) : nullptr;
-        const bool timed = timing && i % every == 0;
-        const size_t k = 2 * (size_t)(i / every);
+    for (uint32_t j = 0; j < nl; ++j) {
+        const uint32_t i0 = first[j], n = first[j + 1] - i0;
+        c->ubo = ubo_of(i0);
+        fill_ubo_args(A, c->ubo);
+        A.nframes = n;
+        for (uint32_t k = 0; k < n; ++k) fill_frame(A.fr[k], ubo_of(i0 + k), frames[i0 + k].out8, frames[i0 + k].in_place);
+        const uint32_t slot = j % nfl;
+        hipStream_t st = sv[slot];
+        if ((rc = prepare_split(c, p, A, slot, st)) != TRT_OK) return rc;
+        const bool timed = timing && j % every == 0;
+        const size_t k = 2 * (size_t)(j / every);
         if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], st));
         HIP_TRY(c, trt::launch_trace(A, st, false));
-        if ((rc = fence_split(c, A, i % nfl, st)) != TRT_OK) return rc;
+        if ((rc = fence_split(c, A, slot, st)) != TRT_OK) return rc;
         if (timed) {
             HIP_TRY(c, hipEventRecord(c->fev[k + 1], st));
-            c->fev_frames = i / every + 1;
+            c->fev_nframes.push_back(n);
+            c->fev_frames = j / every + 1;
         }
     }
+    c->ubo = ubo_of(nframes - 1);
     for (uint32_t k = 0; k + 1 < nfl; ++k) {
         HIP_TRY(c, hipEventRecord(c->aux_ev[k], c->aux[k]));
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->aux_ev[k], 0));
@@ -846,15 +880,44 @@ extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo*
     return TRT_OK;
 }
 
+} // namespace trt
+
+extern "C" int trt_render_frames(trt_ctx* c, const trt_params* p, const trt_ubo* ubos, uint32_t nframes,
+                                 uint8_t* out8, size_t frame_stride, uint32_t time_every) {
+    if (!c) return TRT_ERR_INVALID;
+    if (!p) return fail(c, TRT_ERR_INVALID, "trt_render_frames: null params");
+    std::vector<trt::FrameOut> fl(nframes);
+    const bool in_place = (p->flags & TRT_FLAG_BAND_IN_PLACE) != 0;
+    for (uint32_t i = 0; i < nframes; ++i)
+        fl[i] = trt::FrameOut{ubos ? &ubos[i] : nullptr, out8 ? out8 + (size_t)i * frame_stride : nullptr, in_place};
+    // TRT_FLAG_TIMING: events around every time_every-th launch (0 or 1: every launch)
+    return trt::render_frame_list(c, p, fl.data(), nframes, (p->flags & TRT_FLAG_TIMING) ? std::max(time_every, 1u) : 0u);
+}
+
+extern "C" int trt_set_frame_batch(trt_ctx* c, uint32_t n) {
+    if (!c) return TRT_ERR_INVALID;
+    if (n > TRT_MAX_FRAME_BATCH)
+        return fail(c, TRT_ERR_INVALID, "trt_set_frame_batch: n must be 0 (auto) or in [1, TRT_MAX_FRAME_BATCH]");
+    c->frame_batch = n;
+    return TRT_OK;
+}
+
 extern "C" int trt_frame_times(trt_ctx* c, float* ms, uint32_t n) {
     if (!c || (!ms && n)) return TRT_ERR_INVALID;
-    if (n > c->fev_frames) return fail(c, TRT_ERR_INVALID, "trt_frame_times: more frames than were timed");
+    if (n > c->fev_frames) return fail(c, TRT_ERR_INVALID, "trt_frame_times: more launches than were timed");
     HIP_TRY(c, hipSetDevice(c->device));
     for (uint32_t i = 0; i < n; ++i) {
         HIP_TRY(c, hipEventSynchronize(c->fev[2 * i + 1]));
         HIP_TRY(c, hipEventElapsedTime(&ms[i], c->fev[2 * i], c->fev[2 * i + 1]));
+        ms[i] /= (float)std::max(c->fev_nframes[i], 1u);
     }
     return TRT_OK;
+}
+
+extern "C" uint32_t trt_timed_launches(trt_ctx* c, uint32_t* frames_out, uint32_t cap) {
+    if (!c) return 0;
+    for (uint32_t i = 0; frames_out && i < cap && i < c->fev_frames; ++i) frames_out[i] = c->fev_nframes[i];
+    return c->fev_frames;
 }
 
 extern "C" {
@@ -887,10 +950,10 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     }
     if (out8) {
         if (dev) {
-            A.out8 = reinterpret_cast<uint32_t*>(out8);
+            A.fr[0].out8 = reinterpret_cast<uint32_t*>(out8);
         } else {
             if ((rc = ensure(c, &c->d_out8, &c->cap8, npx * 4, "alloc rgba8")) != TRT_OK) return rc;
-            A.out8 = reinterpret_cast<uint32_t*>(c->d_out8);
+            A.fr[0].out8 = reinterpret_cast<uint32_t*>(c->d_out8);
         }
     }
     if (out32) {

@@ -23,6 +23,36 @@ ROOT_ROTATE = -1  # TRT_ROOT_ROTATE
 ID_BYTES = 128  # TRT_MULTI_ID_BYTES
 
 
+def frame_root(frame: int, nranks: int, root: int) -> int:
+    """trt_frame_root: the rank frame `frame` of a tiled loop is assembled on."""
+    return int(lib().trt_frame_root(int(frame), int(nranks), int(root)))
+
+
+def band_frame_row(k: int, band_rows: int, groups: int, g: int) -> int:
+    """trt_band_frame_row: frame row of compact row k of band group g."""
+    return int(lib().trt_band_frame_row(int(k), int(band_rows), int(groups), int(g)))
+
+
+def band_plan(width: int, height: int, band_rows: int, nranks: int, groups_per_rank: int, first_frame: int,
+              nframes: int, root: int, self_gather: bool = False):
+    """trt_band_plan: (layout, [transfers]) of a tiled batch — the exact exchange
+    trt_render_multi_frames runs over RCCL (host arithmetic, no GPU)."""
+    L = lib()
+    lay = T.BandLayout()
+    n = ctypes.c_uint32()
+    flags = T.PLAN_SELF_GATHER if self_gather else 0
+    args = (int(width), int(height), int(band_rows), int(nranks), int(groups_per_rank), int(first_frame),
+            int(nframes), int(root), flags)
+    rc = L.trt_band_plan(*args, ctypes.byref(lay), None, 0, ctypes.byref(n))
+    if rc != 0:
+        raise TrtError(rc, f"trt_band_plan{args} failed")
+    xs = (T.BandXfer * max(n.value, 1))()
+    rc = L.trt_band_plan(*args, ctypes.byref(lay), xs, n.value, ctypes.byref(n))
+    if rc != 0:
+        raise TrtError(rc, f"trt_band_plan{args} failed")
+    return lay, [xs[i] for i in range(n.value)]
+
+
 def unique_id() -> bytes:
     buf = (ctypes.c_uint8 * ID_BYTES)()
     rc = lib().trt_multi_unique_id(buf)
@@ -101,13 +131,34 @@ class MultiRenderer:
         u = np.ascontiguousarray(ubo)
         self._check(self._L.trt_multi_update_ubo(self._h, u.ctypes.data))
 
-    def _outs(self, outs):
+    def _outs(self, outs, need: int, device: bool):
+        """The C array of output pointers, after checking every given output: contiguous uint8
+        of >= `need` bytes, on the device (torch CUDA) or the host (numpy) as the call needs."""
+        outs = list(outs or [])
+        if len(outs) > self.local_count:
+            raise ValueError(f"{len(outs)} outputs for {self.local_count} local device(s)")
         arr = (ctypes.c_void_p * self.local_count)()
-        for i, o in enumerate(outs or []):
+        for i, o in enumerate(outs):
             if o is None:
                 continue
-            arr[i] = o.data_ptr() if _is_torch_cuda(o) else o.ctypes.data
+            if _is_torch_cuda(o):
+                if not device:
+                    raise ValueError("mixing device and host outputs")
+                ok = o.is_contiguous() and o.dtype.itemsize == 1 and o.numel() >= need
+                arr[i] = o.data_ptr()
+            else:
+                if device or not isinstance(o, np.ndarray):
+                    raise ValueError("outputs must all be torch CUDA tensors or all numpy arrays")
+                ok = o.flags["C_CONTIGUOUS"] and o.dtype == np.uint8 and o.size >= need
+                arr[i] = o.ctypes.data
+            if not ok:
+                raise ValueError(f"output {i} must be contiguous uint8 with >= {need} bytes")
         return arr
+
+    def set_self_gather(self, on: bool) -> None:
+        """trt_multi_set_self_gather: the root's own bands also travel through the gather (the
+        whole exchange on a one-GPU communicator; tests)."""
+        self._check(self._L.trt_multi_set_self_gather(self._h, 1 if on else 0))
 
     def draw_frame(self, params: T.Params, band_rows: int = 8, root: int = 0, outs=None, count: bool = False):
         """One frame gathered on rank `root`.  `outs`: one entry per local device (torch CUDA
@@ -121,24 +172,31 @@ class MultiRenderer:
             p.flags &= ~T.FLAG_DEVICE_PTRS
         if count:
             p.flags |= T.FLAG_COUNT
+        arr = self._outs(outs, p.width * p.height * 4, dev)
         st = T.Stats()
-        self._check(self._L.trt_render_multi(self._h, ctypes.byref(p), int(band_rows), int(root), self._outs(outs),
+        self._check(self._L.trt_render_multi(self._h, ctypes.byref(p), int(band_rows), int(root), arr,
                                              ctypes.byref(st)))
         return st.as_dict()
 
     def render_frames(self, params: T.Params, nframes: int, band_rows: int = 8, root: int = 0,
                       frames_per_gather: int = 1, outs=None, frame_stride: int = 0, ubos=None) -> None:
-        """trt_render_multi_frames into device tensors (enqueue only)."""
+        """trt_render_multi_frames into device tensors (enqueue only).  Frame i lands on rank
+        frame_root(i, ranks, root) at outs[local index] + i * frame_stride bytes."""
         p = T.Params.from_buffer_copy(params)
         p.flags |= T.FLAG_DEVICE_PTRS
         p.flags &= ~(T.FLAG_COUNT | T.FLAG_TIMING)
+        if frame_stride < 0 or frame_stride % 4:
+            raise ValueError("frame_stride must be a non-negative multiple of 4")
+        need = p.width * p.height * 4 + max(int(nframes) - 1, 0) * int(frame_stride)
+        arr = self._outs(outs, need, True)
         u = None
         if ubos is not None:
             u = np.ascontiguousarray(ubos, T.UBO)
-            assert u.shape[0] >= nframes
+            if u.shape[0] < nframes:
+                raise ValueError(f"{u.shape[0]} UBOs for {nframes} frames")
         self._check(self._L.trt_render_multi_frames(
             self._h, ctypes.byref(p), u.ctypes.data if u is not None else None, int(nframes), int(band_rows),
-            int(root), int(frames_per_gather), self._outs(outs), int(frame_stride)))
+            int(root), int(frames_per_gather), arr, int(frame_stride)))
 
     def synchronize(self) -> None:
         self._check(self._L.trt_multi_synchronize(self._h))

@@ -62,6 +62,12 @@ class Renderer:
         deferred-shadow frames)."""
         self._check(self._L.trt_set_frames_in_flight(self._h, int(n)))
 
+    def set_frame_batch(self, n: int) -> None:
+        """Frames per launch of render_frames (trt_set_frame_batch): 0 = auto (up to 64 plain
+        frames per launch), 1 = one launch per frame (the reference's dispatch per frame),
+        2..64."""
+        self._check(self._L.trt_set_frame_batch(self._h, int(n)))
+
     def set_subtree_split(self, window: int) -> None:
         """trt_set_subtree_split: 0 = auto (default), 1 = off, 2..5 = depth window."""
         self._check(self._L.trt_set_subtree_split(self._h, int(window)))
@@ -141,11 +147,12 @@ class Renderer:
 
     def render_frames(self, params: T.Params, out8, nframes: int, ubos: np.ndarray | None = None,
                       frame_stride: int = 0, timing: bool = False, time_every: int = 1) -> int:
-        """Native frame loop (trt_render_frames): `nframes` launches enqueued back to back on
-        the context's stream into the device tensor `out8` (+ i * frame_stride bytes).
+        """Native frame loop (trt_render_frames): `nframes` frames enqueued on the context's
+        stream into the device tensor `out8` (+ i * frame_stride bytes); plain frames go out
+        several per launch (set_frame_batch).
 
-        With `timing`, frames 0, time_every, 2*time_every, ... are bracketed by HIP events;
-        returns how many were (read them with frame_times)."""
+        With `timing`, launches 0, time_every, 2*time_every, ... are bracketed by HIP events;
+        returns how many were (read them with frame_times / launch_frames)."""
         if not _is_torch_cuda(out8):
             raise ValueError("render_frames renders into a device (torch CUDA) tensor")
         p = T.Params.from_buffer_copy(params)
@@ -155,22 +162,31 @@ class Renderer:
             p.flags |= T.FLAG_TIMING
         else:
             p.flags &= ~T.FLAG_TIMING
-        rows = int(self._L.trt_output_rows(ctypes.byref(p)))
-        need = rows * p.width * 4 + (nframes - 1) * frame_stride
-        assert out8.is_contiguous() and out8.numel() >= need
+        rows = p.height if p.flags & T.FLAG_BAND_IN_PLACE else int(self._L.trt_output_rows(ctypes.byref(p)))
+        need = rows * p.width * 4 + max(nframes - 1, 0) * frame_stride
+        if not out8.is_contiguous() or out8.dtype.itemsize != 1 or out8.numel() < need:
+            raise ValueError(f"out8 must be a contiguous uint8 tensor of >= {need} bytes")
         u = None
         if ubos is not None:
             u = np.ascontiguousarray(ubos, T.UBO)
-            assert u.shape[0] >= nframes
+            if u.shape[0] < nframes:
+                raise ValueError(f"{u.shape[0]} UBOs for {nframes} frames")
         self._check(self._L.trt_render_frames(self._h, ctypes.byref(p), u.ctypes.data if u is not None else None,
                                               nframes, out8.data_ptr(), frame_stride, time_every))
-        every = max(1, time_every)
-        return (nframes + every - 1) // every if timing else 0
+        return int(self._L.trt_timed_launches(self._h, None, 0)) if timing else 0
 
     def frame_times(self, n: int) -> np.ndarray:
+        """Device ms per frame of each of the first n timed launches (span / frames traced)."""
         ms = (ctypes.c_float * n)()
         self._check(self._L.trt_frame_times(self._h, ms, n))
         return np.frombuffer(ms, np.float32).copy()
+
+    def launch_frames(self) -> np.ndarray:
+        """Frames traced by each launch timed by the last timed render_frames call."""
+        n = int(self._L.trt_timed_launches(self._h, None, 0))
+        out = (ctypes.c_uint32 * max(n, 1))()
+        self._L.trt_timed_launches(self._h, out, n)
+        return np.frombuffer(out, np.uint32)[:n].copy()
 
     # -- envmap JPEG (SURVEY §8 f2) -----------------------------------------------------------
     def decode_jpeg(self, jpeg, out=None):

@@ -100,6 +100,19 @@ def make_ubo(cam=(0.0, 0.0, 0.0), spheres=SPHERES, lights=LIGHTS) -> np.ndarray:
     return u
 
 
+def camera_path(ubo: np.ndarray, n: int, speed: float = 0.02) -> np.ndarray:
+    """n per-frame UBOs of the reference's interactive loop with W and D held: processInput
+    (main.cpp:391-403) moves cameraPos by cameraSpeed along cameraFront (0, 0, -1) and along
+    normalize(cross(cameraFront, cameraUp)) = (1, 0, 0) every frame, and updateUniformBuffer
+    (main.cpp:2165-2179) writes it to the frame's UBO.  cameraSpeed = 5 / FPS in the reference;
+    `speed` fixes it per frame."""
+    out = np.repeat(ubo[None], n, axis=0).copy()
+    base = np.array(ubo["camPos"][:3], np.float32)
+    for k in range(n):
+        out[k]["camPos"][:3] = base + np.float32(speed) * np.array([k, 0.0, -k], np.float32)
+    return out
+
+
 # ---- synthetic inputs --------------------------------------------------------------------
 
 

@@ -136,7 +136,39 @@ class Stats(ctypes.Structure):
         return d
 
 
+class BandLayout(ctypes.Structure):
+    """trt_band_layout (abi.h): buffer shapes of a tiled batch."""
+
+    _fields_ = [
+        ("groups", ctypes.c_uint32),
+        ("max_rows", ctypes.c_uint32),
+        ("block_bytes", ctypes.c_uint64),
+        ("local_bytes", ctypes.c_uint64),
+        ("gather_bytes", ctypes.c_uint64),
+    ]
+
+
+class BandXfer(ctypes.Structure):
+    """trt_band_xfer (abi.h): one compact band buffer travelling to a frame's root."""
+
+    _fields_ = [
+        ("frame", ctypes.c_uint32),
+        ("group", ctypes.c_uint32),
+        ("src", ctypes.c_uint32),
+        ("dst", ctypes.c_uint32),
+        ("rows", ctypes.c_uint32),
+        ("slot", ctypes.c_uint32),
+        ("src_offset", ctypes.c_uint64),
+        ("dst_offset", ctypes.c_uint64),
+        ("bytes", ctypes.c_uint64),
+    ]
+
+
+PLAN_SELF_GATHER = 1  # TRT_PLAN_SELF_GATHER
+ROOT_ROTATE = -1  # TRT_ROOT_ROTATE
+
 assert ctypes.sizeof(Params) == 48 and ctypes.sizeof(Stats) == 168
+assert ctypes.sizeof(BandLayout) == 32 and ctypes.sizeof(BandXfer) == 48
 
 
 def make_params(
