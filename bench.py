@@ -315,20 +315,26 @@ def frame_loop(dev: int, scene, frames: int, warmup: int, args, g: Group | None 
         r.set_frames_in_flight(args.inflight)
         r.set_frame_batch(args.frame_batch)
         r.render_frames(p, out8, max(1, min(warmup, ring)), ubos=ubos, frame_stride=fb)
-        box = {"ms": [], "nf": []}
+        chunks = [(i0, min(ring, frames - i0)) for i0 in range(0, frames, ring)]
+        ubo_chunks = [np.ascontiguousarray(ubos[i0:i0 + n]) for i0, n in chunks]
 
         def run():
-            for i0 in range(0, frames, ring):
-                n = min(ring, frames - i0)
-                nt = r.render_frames(p, out8, n, ubos=ubos[i0:i0 + n], frame_stride=fb, timing=True)
-                box["ms"].append(r.frame_times(nt))
-                box["nf"].append(r.launch_frames())
+            for (_, n), u in zip(chunks, ubo_chunks):
+                r.render_frames(p, out8, n, ubos=u, frame_stride=fb)
 
         elapsed = timed(g or Group(1, 0), run)
-        ms = np.concatenate(box["ms"])
-        nf = np.concatenate(box["nf"]).astype(np.float64)
+        # the same loop again with HIP events around every launch (outside the timed region):
+        # the device time per frame of the launches
+        ms, nf = [], []
+        for (_, n), u in zip(chunks, ubo_chunks):
+            nt = r.render_frames(p, out8, n, ubos=u, frame_stride=fb, timing=True)
+            ms.append(r.frame_times(nt))
+            nf.append(r.launch_frames())
+        ms = np.concatenate(ms)
+        nf = np.concatenate(nf).astype(np.float64)
         kernel_ms_per_frame = float((ms * nf).sum() / nf.sum())  # launch spans / frames
         launches = int(len(nf))
+        torch.cuda.synchronize()
         ok = None
         if check_last:
             last = frames - 1
@@ -343,9 +349,11 @@ def frame_loop(dev: int, scene, frames: int, warmup: int, args, g: Group | None 
         r.close()
 
 
-def auto_per_gather(total: int, arg: int) -> int:
+def auto_per_gather(total: int, world: int, arg: int) -> int:
     if arg > 0:
         return arg
+    if world == 1:  # nothing travels at one rank: one batch of multi-frame launches
+        return max(1, min(64, total))
     return max(1, min(64, -(-total // 4)))  # >= 4 exchanges pipeline in the timed region
 
 
@@ -372,17 +380,19 @@ def tiled_loop(g: Group, dev: int, multi, scene, frames: int, warmup: int, args,
     ubos = np.stack([wk[i % len(wk)] for i in range(frames)])
     fb = p.height * p.width * 4
     out = torch.zeros((ring, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before the frames
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
     # warmup: one exchange of the timed size, so the timed batches never allocate
     multi.render_frames(p, max(min(warmup, ring), min(per_gather, ring)), args.band_rows, root, per_gather,
                         outs=[out], frame_stride=fb, ubos=ubos)
 
+    chunks = [(i0, min(ring, frames - i0)) for i0 in range(0, frames, ring)]
+    ubo_chunks = [np.ascontiguousarray(ubos[i0:i0 + n]) for i0, n in chunks]
+
     def run():
-        for i0 in range(0, frames, ring):
-            n = min(ring, frames - i0)
-            multi.render_frames(p, n, args.band_rows, root, per_gather, outs=[out], frame_stride=fb,
-                                ubos=ubos[i0:i0 + n])
+        for (_, n), u in zip(chunks, ubo_chunks):
+            multi.render_frames(p, n, args.band_rows, root, per_gather, outs=[out], frame_stride=fb, ubos=u)
 
     elapsed = timed(g, run)
     multi.set_stream(0, None)
@@ -444,6 +454,7 @@ def tiled_frame(g: Group, dev: int, multi, frames: int, args) -> dict | None:
     multi.upload_scene(sc if g.rank == 0 else None)
     st = multi.draw_frame(p, band_rows=args.band_rows, root=0, count=True)
     out = torch.zeros((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
     multi.render_frames(p, 2, args.band_rows, 0, 1, outs=[out])
@@ -522,7 +533,7 @@ def main():
     multi = MultiRenderer.for_rank(dev, world, rank, g.unique_id())
     # the tiled loop: N frames per step (weak), each row-tiled over all N GPUs, rotating roots
     t_frames = K * world
-    fpg = auto_per_gather(t_frames, args.frames_per_gather)
+    fpg = auto_per_gather(t_frames, world, args.frames_per_gather)
     el_t, rays_t, mean_t, tiled_ok = tiled_loop(g, dev, multi, scene, t_frames, args.warmup, args, fpg, ROOT_ROTATE)
     tiled_value = rays_t / el_t / 1e6
     tiled = {
@@ -550,7 +561,7 @@ def main():
             "workload": f"every rank renders its own whole {args.config} frames, no data-path collective",
             "last_frame_ok": plain_ok}
         # strong form: one frame per step over all N GPUs
-        fpg1 = auto_per_gather(K, args.frames_per_gather)
+        fpg1 = auto_per_gather(K, world, args.frames_per_gather)
         el_s, rays_s, _, ok_s = tiled_loop(g, dev, multi, scene, K, args.warmup, args, fpg1, ROOT_ROTATE)
         extra["strong_scaling"] = {
             "value": round(rays_s / el_s / 1e6, 3), "unit": "Mray/s", "ms_per_step": round(el_s / K * 1e3, 5),
@@ -580,7 +591,8 @@ def main():
         rl["note"] = ("FP32 flops of one frame's executed work in SURVEY §8d units (counting passes of the camera "
                       "walk, mean per frame) / the wall time per frame of the timed loop (at N > 1: per GPU); "
                       "kernel_us_per_frame = HIP-event span of every launch / the frames it traced (one launch "
-                      "traces many frames).  Peak counts an FMA as 2 flops; the kernel has no FMA contraction "
+                      "traces many frames), from a second, untimed pass of the same loop.  Peak counts an FMA "
+                      "as 2 flops; the kernel has no FMA contraction "
                       "(-ffp-contract=off).  traffic: no PMC pass in this run (profiles/ holds this build's PMC "
                       "summaries)")
         result = {

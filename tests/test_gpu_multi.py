@@ -86,6 +86,7 @@ def test_self_gather_frame_batches(gpu_renderer, multi, config, groups, band_row
     want = _single_frames(gpu_renderer, sc, p, ubos)
     fb = p.height * p.width * 4
     out = torch.zeros((n, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     stream = torch.cuda.Stream()
     multi.set_band_groups(groups)
     multi.set_self_gather(True)
@@ -116,6 +117,7 @@ def test_render_multi_frames_device_batches(gpu_renderer, multi, self_gather):
     multi.upload_scene(sc)
     p = sc.params()
     out = torch.zeros((7, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
     try:
@@ -145,6 +147,7 @@ def test_render_multi_frames_first_batches_after_upload():
         r.upload_scene(sc)
         want, _, _ = r.draw_frame(p)
     out = torch.zeros((4, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     with MultiRenderer([0]) as m:
         m.upload_scene(sc)
         m.render_frames(p, 4, band_rows=8, root=0, frames_per_gather=1, outs=[out],
@@ -169,6 +172,7 @@ def test_render_multi_deep_mesh_frames(gpu_renderer, multi, golden_meshes, self_
     multi.set_self_gather(self_gather)
     multi.upload_scene(sc)
     out = torch.zeros((4, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     try:
         multi.render_frames(p, 4, band_rows=8, root=ROOT_ROTATE, frames_per_gather=2, outs=[out],
                             frame_stride=p.height * p.width * 4, ubos=ubos)
@@ -220,6 +224,7 @@ def test_render_multi_errors(multi):
     with pytest.raises(ValueError):
         multi.draw_frame(p, outs=[np.zeros((48, 64, 4), np.float32)])  # wrong dtype
     small = torch.zeros((2, 48, 64, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     with pytest.raises(ValueError):  # 3 frames do not fit 2 frames' worth of bytes
         multi.render_frames(p, 3, outs=[small], frame_stride=48 * 64 * 4)
     with pytest.raises(ValueError):

@@ -152,6 +152,7 @@ def test_bands_in_place_assemble_the_frame(gpu_renderer, golden_meshes, which):
     full, full32, _ = gpu_renderer.draw_frame(sc.params(), want32=True)
     out8 = torch.zeros((sc.height, sc.width, 4), dtype=torch.uint8, device="cuda")
     out32 = torch.zeros((sc.height, sc.width, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     for idx in range(3):
         p = sc.params(band_rows=8, band_count=3, band_index=idx)
         p.flags |= T.FLAG_BAND_IN_PLACE
@@ -255,6 +256,7 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
     gpu_renderer.upload_scene(sc)
     ubos = np.stack([S.make_ubo(cam=(0.1 * i, 0.0, -0.2 * i)) for i in range(4)])
     out = torch.zeros((4, 64, 96, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     stream = torch.cuda.Stream()
     gpu_renderer.set_stream(stream)
     try:
@@ -324,6 +326,7 @@ def test_multi_frame_launches_match_single_frames(gpu_renderer, config, sphere_e
     ubos = _moving_ubos(n, sphere_every)
     fb = p.height * p.width * 4
     out = torch.zeros((n, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     stream = torch.cuda.Stream()
     gpu_renderer.set_stream(stream)
     try:
@@ -337,8 +340,8 @@ def test_multi_frame_launches_match_single_frames(gpu_renderer, config, sphere_e
         gpu_renderer.set_frames_in_flight(0)
         gpu_renderer.set_stream(None)
     assert int(launches.sum()) == n
-    # frames per launch: ceil(n / in-flight slots), at most the batch size (auto slots: 4)
-    per = max(1, min(batch or 64, -(-n // (inflight or 4))))
+    # frames per launch: ceil(n / in-flight slots), at most the batch size (auto: one slot)
+    per = max(1, min(batch or 64, -(-n // (inflight or 1))))
     assert launches.max() <= per
     if sphere_every:
         assert len(launches) >= (n + sphere_every - 1) // sphere_every
@@ -370,6 +373,7 @@ def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
     n = 9
     ubos = np.stack([S.make_ubo(cam=(0.07 * i, 0.02 * i, -0.1 * i)) for i in range(n)])
     out = torch.zeros((n, 64, 96, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     stream = torch.cuda.Stream()
     gpu_renderer.set_stream(stream)
     try:

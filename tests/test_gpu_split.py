@@ -102,6 +102,7 @@ def test_split_with_frames_in_flight(gpu_renderer, scenes, defer):
     n, H, W = 5, sc.height, sc.width
     ubos = np.stack([S.make_ubo(cam=(0.03 * i, 0.0, -0.05 * i)) for i in range(n)])
     out = torch.zeros((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on the default stream: order it before our streams
     stream = torch.cuda.Stream()
     gpu_renderer.set_stream(stream)
     try:

@@ -4,8 +4,8 @@
 # per frame and kernel span per frame).
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 for steps in 20 1000; do
-  for fl in ${INFLIGHTS:-2 4 8}; do
-    for fb in ${BATCHES:-0 1}; do
+  for fl in ${INFLIGHTS:-1 2 3 4}; do
+    for fb in ${BATCHES:-0 1 8}; do
       out=$(timeout -k 10 120 python bench.py --steps $steps --warmup 5 --no-cpu --extra-frames 0 --tiled-frames 0 \
             --inflight $fl --frame-batch $fb 2>/dev/null | tail -1)
       rc=$?

@@ -100,6 +100,10 @@ constexpr size_t kPersistWords = 8 * 32; // 8 XCDs x (ticket, done) on their own
 
 namespace trt {
 
+// A 4-byte fill on a new stream (then a sync), so its hardware queue is created now instead of
+// at its first frame.
+hipError_t touch_stream(hipStream_t s, void* scratch);
+
 // One frame of a frame loop: its UBO (null: the context's current one), its RGBA8 image (a
 // device pointer, or null) and whether a band launch writes its rows at their frame rows.
 struct FrameOut {

@@ -167,6 +167,7 @@ int init_dev(trt_multi* m, trt_multi::Dev& d) {
     MHIP(m, hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
     MHIP(m, hipEventCreateWithFlags(&d.join, hipEventDisableTiming));
     MHIP(m, hipMalloc(&d.scratch, kScratchBytes));
+    for (hipStream_t s : {d.comm_stream, d.render[0], d.render[1]}) MHIP(m, trt::touch_stream(s, d.scratch));
     return TRT_OK;
 }
 
@@ -692,6 +693,25 @@ int trt_render_multi_frames(trt_multi* m, const trt_params* p, const trt_ubo* ub
         return mfail(m, TRT_ERR_INVALID, "trt_render_multi_frames: COUNT/TIMING are trt_render_multi flags");
     if (frame_stride % 4) return mfail(m, TRT_ERR_INVALID, "frame_stride must be a multiple of 4");
     const uint32_t F = std::min(std::max(frames_per_gather, 1u), TRT_MAX_FRAME_BATCH);
+    if (m->nranks == 1 && !m->self_gather) {
+        // One rank: nothing travels and nothing is re-interleaved, so the tiled loop is the frame
+        // loop — each band group traced in place on the context's stream, no batch streams, no
+        // events (each cross-stream hop costs ~10 us of GPU latency and a few HIP calls).
+        auto& d = m->devs[0];
+        const uint32_t NG = m->groups;
+        std::vector<trt::FrameOut> fl(nframes);
+        for (uint32_t v = 0; v < NG; ++v) {
+            trt_params q = group_params(p, band_rows, NG, v);
+            q.flags &= ~(TRT_FLAG_COUNT | TRT_FLAG_TIMING);
+            if (!trt_output_rows(&q)) continue;
+            for (uint32_t i = 0; i < nframes; ++i)
+                fl[i] = trt::FrameOut{ubos ? &ubos[i] : nullptr,
+                                      (out8 && out8[0]) ? out8[0] + (size_t)i * frame_stride : nullptr, NG > 1};
+            if ((rc = trt::render_frame_list(d.ctx, &q, fl.data(), nframes, 0)) != TRT_OK)
+                return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
+        }
+        return TRT_OK;
+    }
     if ((rc = fork_all(m)) != TRT_OK) return rc;
     std::vector<uint8_t*> outs(m->devs.size());
     for (uint32_t i0 = 0; i0 < nframes; i0 += F) {

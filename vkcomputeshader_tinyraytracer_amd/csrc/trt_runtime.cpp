@@ -27,6 +27,13 @@
 #include "trt_device.h"
 
 namespace trt {
+// HIP creates a stream's hardware queue at its first submission, which costs ~0.1 ms: every
+// stream the library creates gets a 4-byte fill of scratch memory (then a sync) right away, so
+// that cost never lands in a frame loop.
+hipError_t touch_stream(hipStream_t s, void* scratch) {
+    hipError_t e = hipMemsetAsync(scratch, 0, 4, s);
+    return e == hipSuccess ? hipStreamSynchronize(s) : e;
+}
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
 hipError_t launch_envp(const uint32_t* env, uint2* out, uint32_t W, uint32_t H, hipStream_t stream);
 hipError_t launch_shadow_batch(const KArgs& A, const float4* rays, uint32_t n, uint32_t* occ, hipStream_t stream);
@@ -197,6 +204,10 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = (uint32_t)prop.multiProcessorCount;
     c->stream = c->own_stream;
+    if (trt::touch_stream(c->own_stream, c->d_counters) != hipSuccess) {
+        trt_destroy(c);
+        return TRT_ERR_HIP;
+    }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
     *out = c;
     return TRT_OK;
@@ -810,14 +821,15 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     const bool plain = !defer && !split;
     // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): launch j runs on slot j % n.  Slot 0
     // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
-    // joined back into it below, so to the caller all frames complete on its stream.  Auto: 4
-    // (C2 -13 % at 4 vs 2, profiles/r02_ab_queues_c2.log), or 8 for deferred-shadow frames (the
-    // shipped frame 1.45 -> 0.56 ms at 8, r02_ab_queues_deep.log).  Each slot is a hardware
-    // queue with its own dispatcher: a C2 frame's 12,288 one-wave workgroups are
-    // dispatch-limited on one queue (16.5 us per frame inside one multi-frame launch against
-    // 13.8 us with 4 queues feeding the GPU), so a plain loop spreads its multi-frame launches
-    // over the slots: ceil(nframes / slots) frames per launch, at most frame_batch.
-    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : defer ? 8u : 4u;
+    // joined back into it below, so to the caller all frames complete on its stream.  A plain
+    // loop needs no second slot: one multi-frame launch keeps the GPU full from its first frame
+    // to its last, so a 20-frame loop is one launch and drains once (C2 at 20 frames: 20.5 us per
+    // frame against 25.0 with one launch per frame on 4 slots; at 1000 frames 15.6 vs 15.9,
+    // profiles/r03_ab_frame_batch.log); with n slots set explicitly the frames are spread over
+    // n launches.  Per-frame launch sequences (split / deferred-shadow frames) keep the slots
+    // busy instead: auto 4, or 8 for deferred-shadow frames (the shipped frame 1.45 -> 0.56 ms at
+    // 8, profiles/r02_ab_queues_deep.log).
+    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : plain ? 1u : defer ? 8u : 4u;
     const uint32_t cap = plain ? (c->frame_batch ? c->frame_batch : trt::kMaxLaunchFrames) : 1u;
     const uint32_t per_launch = std::max(1u, std::min(cap, (nframes + want - 1) / want));
     // launches: runs of consecutive frames sharing every UBO field but camPos
@@ -836,15 +848,19 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     }
     const uint32_t nfl = std::min(want, nl);
     std::vector<hipStream_t> sv{c->stream};
+    // every slot's stream is made on first use of the in-flight count, not only the ones this
+    // call needs: creating a stream takes milliseconds and must not land in a later, longer
+    // call (a timed loop after a short warmup)
+    while (c->aux.size() + 1 < want) {
+        hipStream_t s;
+        HIP_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIP_TRY(c, trt::touch_stream(s, c->d_counters)); // its hardware queue exists from now on
+        c->aux.push_back(s);
+        hipEvent_t e;
+        HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->aux_ev.push_back(e);
+    }
     if (nfl > 1) {
-        while (c->aux.size() < nfl - 1) {
-            hipStream_t s;
-            HIP_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-            c->aux.push_back(s);
-            hipEvent_t e;
-            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            c->aux_ev.push_back(e);
-        }
         if (!c->fork_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->fork_ev, c->stream));
         for (uint32_t k = 0; k + 1 < nfl; ++k) {
