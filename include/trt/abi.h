@@ -318,13 +318,18 @@ int trt_multi_set_self_gather(trt_multi* m, int on);
  * at frame `first_frame` of the call, as a list of transfers, so a host with its own transport
  * (MPI, torch.distributed, ...) can run the same exchange; trt_multi.cpp executes exactly this
  * plan over RCCL (ncclSend / ncclRecv in list order on both ends, one group).  Frame i's root is
- * trt_frame_root(i, nranks, root): `root`, or i % nranks for TRT_ROOT_ROTATE.  Rank r renders
- * band groups r * groups_per_rank .. + groups_per_rank - 1 of every frame; a group's rows
- * of frame f are stored compactly at (f * groups_per_rank + v) * block_bytes of the rank's
- * batch buffer; a root receives them at (j * groups + g) * block_bytes of its gather buffer, j
- * = the frame's index among the batch frames it roots; then compact row k of group g is frame
- * row trt_band_frame_row(k, band_rows, groups, g).  Without TRT_PLAN_SELF_GATHER the root's own
- * groups do not travel (it renders them in place).  Pure host arithmetic (no GPU). */
+ * trt_frame_root(i, nranks, root): `root`, or i % nranks for TRT_ROOT_ROTATE.  Rank q renders
+ * band groups q * G .. q * G + G - 1 (G = groups_per_rank) of every frame.  One transfer per
+ * (sender, root) pair carries all of the batch's frames that root owns:
+ *   - the batch frames are ordered by root; rank r's J_r frames (batch order) start at frame
+ *     slot off_r = the number of batch frames rooted by ranks < r;
+ *   - a sender stores group v of the j-th frame of root r at ((off_r + j) * G + v) * block_bytes
+ *     of its batch buffer, so the J_r * G blocks for root r are contiguous;
+ *   - root r receives sender q's blocks at (q * J_r * G) * block_bytes of its gather buffer, i.e.
+ *     group v of its j-th frame at ((q * J_r + j) * G + v) * block_bytes;
+ *   - compact row k of band group g is frame row trt_band_frame_row(k, band_rows, groups, g).
+ * Blocks are block_bytes each (padded to the largest group).  Without TRT_PLAN_SELF_GATHER the
+ * root's own groups do not travel (it renders them in place).  Pure host arithmetic. */
 typedef struct trt_band_layout {
     uint32_t groups;       /* band groups NG = nranks * groups_per_rank */
     uint32_t max_rows;     /* compact rows of the largest group */
@@ -333,14 +338,14 @@ typedef struct trt_band_layout {
     uint64_t gather_bytes; /* the largest gather buffer of a root: frames rooted * groups * block_bytes */
 } trt_band_layout;
 typedef struct trt_band_xfer {
-    uint32_t frame;      /* frame of the batch (0 .. nframes-1) */
-    uint32_t group;      /* global band group */
-    uint32_t src, dst;   /* sending rank (group / groups_per_rank), receiving rank (the frame's root) */
-    uint32_t rows;       /* compact rows of the group */
-    uint32_t slot;       /* the frame's index among the batch frames `dst` roots */
-    uint64_t src_offset; /* bytes into the sender's batch buffer */
-    uint64_t dst_offset; /* bytes into the root's gather buffer */
-    uint64_t bytes;      /* rows * width * 4 */
+    uint32_t src, dst;   /* sending rank, receiving rank (the root of the carried frames) */
+    uint32_t frames;     /* J_dst: the batch frames dst roots (all of them travel together) */
+    uint32_t groups;     /* band groups per frame (groups_per_rank) */
+    uint32_t first_slot; /* off_dst: their first frame slot in the sender's buffer */
+    uint32_t pad;
+    uint64_t src_offset; /* bytes into the sender's batch buffer: off_dst * G * block_bytes */
+    uint64_t dst_offset; /* bytes into the root's gather buffer: src * J_dst * G * block_bytes */
+    uint64_t bytes;      /* J_dst * G * block_bytes */
 } trt_band_xfer;
 #define TRT_PLAN_SELF_GATHER 1u
 uint32_t trt_frame_root(uint32_t frame, uint32_t nranks, int root);

@@ -18,10 +18,16 @@ import numpy as np
 #    GPU, each within ~1-2 ulp).  The worst case is the envmap lookup: 2 ulp of u times the
 #    7616-texel width moves the bilinear weight by ~2e-3 of one texel step, i.e. <= ~2e-3 of
 #    full scale before gamma, <= 2.2x that after.  5e-3 (~1.3 LSB of 8-bit) bounds it.
+#
+# Measured use of the bar (profiles/r03_parity_log_a.jsonl: 70 RGBA8 and 46 rayOut comparisons
+# of the GPU suite, round 3): max |d| = 1, worst differing-pixel fraction 0.37 %
+# (test_flag_combinations[FLOOR]), worst rayOut error 4.3e-4 (C2 at the 7616x3808 envmap).  The
+# bar is set at about twice the measured worst case: 0.8 % of pixels, 1e-3 per float (the
+# derivation above bounds the float error by 5e-3).
 RGBA8_TOL = 1
-FLOAT_TOL = 5e-3
+FLOAT_TOL = 1e-3
 # Largest fraction of pixels allowed to differ (by at most RGBA8_TOL).
-MAX_FRAC = 0.02
+MAX_FRAC = 0.008
 
 
 def diff_report(a8: np.ndarray, b8: np.ndarray) -> dict:

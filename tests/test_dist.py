@@ -116,8 +116,9 @@ def test_band_partition(H, band_rows, world):
     (1024, 768, 8, 1, 1, 4, ROOT_ROTATE, True),
 ])
 def test_band_plan_invariants(W, H, B, N, G, F, root, self_gather):
-    """The plan delivers every row of every frame to the frame's root exactly once (the root's
-    own groups in place unless self_gather), within the buffers it sizes, without overlaps."""
+    """The plan moves, for every frame, every non-empty band group of every other rank (and the
+    root's own with self_gather) to the frame's root exactly once, in one transfer per (sender,
+    root) pair whose byte ranges stay inside the buffers the layout sizes and do not overlap."""
     lay, plan = band_plan(W, H, B, N, G, 0, F, root, self_gather)
     NG = N * G
     assert lay.groups == NG
@@ -125,33 +126,41 @@ def test_band_plan_invariants(W, H, B, N, G, F, root, self_gather):
     assert lay.local_bytes == F * G * lay.block_bytes
     rows_of = [len(T.output_rows(H, B, NG, g)) if NG > 1 else H for g in range(NG)]
     assert lay.max_rows == max(rows_of)
-    delivered = {}
-    src_used, dst_used = {}, {}
+    roots = [frame_root(f, N, root) for f in range(F)]
+    J = [roots.count(r) for r in range(N)]
+    off = [sum(J[:r]) for r in range(N)]
+    pairs = set()
     for x in plan:
-        r = frame_root(x.frame, N, root)
-        assert x.dst == r and x.src == x.group // G
+        assert (x.src, x.dst) not in pairs  # one transfer per (sender, root)
+        pairs.add((x.src, x.dst))
         assert x.src != x.dst or self_gather
-        assert x.rows == rows_of[x.group] > 0 and x.bytes == x.rows * W * 4
-        assert x.src_offset == (x.frame * G + x.group % G) * lay.block_bytes
+        assert x.frames == J[x.dst] > 0 and x.groups == G and x.first_slot == off[x.dst]
+        assert x.bytes == J[x.dst] * G * lay.block_bytes
+        assert x.src_offset == off[x.dst] * G * lay.block_bytes
+        assert x.dst_offset == x.src * J[x.dst] * G * lay.block_bytes
         assert x.src_offset + x.bytes <= lay.local_bytes
         assert x.dst_offset + x.bytes <= lay.gather_bytes
-        key = (x.frame, x.group)
-        assert key not in delivered
-        delivered[key] = x
-        for used, who, off in ((src_used, x.src, x.src_offset), (dst_used, x.dst, x.dst_offset)):
-            assert (who, off) not in used
-            used[(who, off)] = True
+    # every frame's every group reaches the frame's root exactly once
     for f in range(F):
-        r = frame_root(f, N, root)
+        r = roots[f]
         for g in range(NG):
-            own = g // G == r
-            if rows_of[g] == 0 or (own and not self_gather):
-                assert (f, g) not in delivered
+            q = g // G
+            moved = (q, r) in pairs
+            if q == r and not self_gather:
+                assert not moved
             else:
-                assert (f, g) in delivered
+                assert moved
+    # a sender's ranges for different roots, and a root's ranges from different senders, are disjoint
+    for who in ("src", "dst"):
+        for k in range(N):
+            spans = sorted(((x.src_offset, x.bytes) if who == "src" else (x.dst_offset, x.bytes))
+                           for x in plan if getattr(x, who) == k)
+            for (a, n), (b, _) in zip(spans, spans[1:]):
+                assert a + n <= b
     # with a rotating root every device roots ceil(F / N) frames at most
     if root == ROOT_ROTATE:
         assert lay.gather_bytes == -(-F // N) * NG * lay.block_bytes
+    assert len(plan) == sum(1 for r in range(N) if J[r] for q in range(N) if q != r or self_gather)
 
 
 def test_band_plan_rejects_bad_shapes():

@@ -9,7 +9,7 @@ mkdir -p "$OUT" "$ROOT/build/diag"
 FP="-ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math -fno-slp-vectorize"
 HOST="-O2 -std=c++17 -fPIC -ffp-contract=off -I/opt/rocm/include -D__HIP_PLATFORM_AMD__"
 HDR_NEWEST=$(ls -t "$SRC"/*.h "$ROOT"/include/trt/*.h | head -n 1)
-for f in trt_runtime trt_multi scene_build obj_load bvh_build image_io jpeg_entropy jpeg_api; do
+for f in trt_runtime trt_multi band_plan scene_build obj_load bvh_build image_io jpeg_entropy jpeg_api; do
     [ "$ROOT/build/diag/$f.o" -nt "$SRC/$f.cpp" ] && [ "$ROOT/build/diag/$f.o" -nt "$HDR_NEWEST" ] || /opt/rocm/bin/hipcc $HOST -x c++ -c -o "$ROOT/build/diag/$f.o" "$SRC/$f.cpp"
 done
 variant() { # name extra-flags...
@@ -18,7 +18,7 @@ variant() { # name extra-flags...
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "$@" -c -o "$ROOT/build/diag/k_$name.o" "${KSRC:-$SRC/trt_kernel.hip}"
     [ "$ROOT/build/diag/jpeg_kernel.o" -nt "$SRC/jpeg_kernel.hip" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -c -o "$ROOT/build/diag/jpeg_kernel.o" "$SRC/jpeg_kernel.hip"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libtrt_$name.so" "$ROOT/build/diag/k_$name.o" \
-        "$ROOT/build/diag/trt_runtime.o" "$ROOT/build/diag/trt_multi.o" "$ROOT/build/diag/scene_build.o" "$ROOT/build/diag/obj_load.o" \
+        "$ROOT/build/diag/trt_runtime.o" "$ROOT/build/diag/trt_multi.o" "$ROOT/build/diag/band_plan.o" "$ROOT/build/diag/scene_build.o" "$ROOT/build/diag/obj_load.o" \
         "$ROOT/build/diag/bvh_build.o" "$ROOT/build/diag/image_io.o" "$ROOT/build/diag/jpeg_entropy.o" \
         "$ROOT/build/diag/jpeg_api.o" "$ROOT/build/diag/jpeg_kernel.o" -lz -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
     echo "built $OUT/libtrt_$name.so"
@@ -26,6 +26,7 @@ variant() { # name extra-flags...
 for v in "$@"; do
     case $v in
         base) variant base ;;
+        unode) variant unode -DTRT_UNIFORM_NODE=1 ;;
         noquant) variant noquant -DTRT_BVH_QUANT=0 ;;
         noskip) variant noskip -DTRT_SKIP_DARK=0 ;;
         dumpshadow) variant dumpshadow -DTRT_DIAG_DUMP_SHADOW ;;

@@ -60,8 +60,8 @@ def main():
     r.set_subtree_split(a.split)
     r.set_deferred_shadows(a.defer)
     r.render_frames(p, out, 5)
-    r.render_frames(p, out, a.frames, timing=True)
-    ms = r.frame_times(a.frames)
+    nt = r.render_frames(p, out, a.frames, timing=True)
+    ms = r.frame_times(nt)  # per frame of each launch
     torch.cuda.synchronize()
     # wall per frame of a back-to-back batch without per-frame events (one event pair)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

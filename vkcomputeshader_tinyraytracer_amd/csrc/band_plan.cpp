@@ -25,36 +25,47 @@ int build_band_plan(uint32_t W, uint32_t H, uint32_t B, uint32_t N, uint32_t G, 
     for (uint32_t g = 0; g < NG; ++g) L.max_rows = std::max(L.max_rows, band_group_rows(H, B, NG, g));
     L.block_bytes = (uint64_t)L.max_rows * W * 4;
     L.local_bytes = (uint64_t)F * G * L.block_bytes;
-    // frames rooted by each rank, and each frame's index among its root's frames
-    std::vector<uint32_t> rooted(N, 0), slot(F);
-    for (uint32_t f = 0; f < F; ++f) {
-        const uint32_t r = trt_frame_root(first + f, N, root);
-        slot[f] = rooted[r]++;
-    }
+    std::vector<uint32_t> rooted(N, 0);
+    for (uint32_t f = 0; f < F; ++f) ++rooted[trt_frame_root(first + f, N, root)];
     L.gather_bytes = (uint64_t)*std::max_element(rooted.begin(), rooted.end()) * NG * L.block_bytes;
     if (!xfers) return TRT_OK;
     xfers->clear();
+    // one transfer per (sender, root): every batch frame the root owns, all of the sender's
+    // groups, contiguous on both ends (per-transfer overhead, not bytes, dominated the
+    // per-frame, per-group exchange: profiles/r03_exchange_probe_per_group_transfers.log)
     const bool self = (flags & TRT_PLAN_SELF_GATHER) != 0;
-    for (uint32_t f = 0; f < F; ++f) {
-        const uint32_t r = trt_frame_root(first + f, N, root);
-        for (uint32_t g = 0; g < NG; ++g) {
-            const uint32_t src = g / G, v = g % G;
-            const uint32_t rows = band_group_rows(H, B, NG, g);
-            if (!rows || (src == r && !self)) continue;
-            trt_band_xfer x{};
-            x.frame = f;
-            x.group = g;
-            x.src = src;
-            x.dst = r;
-            x.rows = rows;
-            x.slot = slot[f];
-            x.src_offset = ((uint64_t)f * G + v) * L.block_bytes;
-            x.dst_offset = ((uint64_t)slot[f] * NG + g) * L.block_bytes;
-            x.bytes = (uint64_t)rows * W * 4;
-            xfers->push_back(x);
-        }
+    uint32_t off = 0;
+    for (uint32_t r = 0; r < N; ++r) {
+        const uint32_t J = rooted[r];
+        if (J)
+            for (uint32_t q = 0; q < N; ++q) {
+                if (q == r && !self) continue;
+                trt_band_xfer x{};
+                x.src = q;
+                x.dst = r;
+                x.frames = J;
+                x.groups = G;
+                x.first_slot = off;
+                x.src_offset = (uint64_t)off * G * L.block_bytes;
+                x.dst_offset = (uint64_t)q * J * G * L.block_bytes;
+                x.bytes = (uint64_t)J * G * L.block_bytes;
+                xfers->push_back(x);
+            }
+        off += J;
     }
     return TRT_OK;
+}
+
+// Frame slots of a batch: frames ordered by root, so slot[f] = off_root(f) + (the frame's index
+// among its root's frames); j[f] = that index.
+void band_plan_slots(uint32_t N, uint32_t first, uint32_t F, int root, std::vector<uint32_t>& slot,
+                     std::vector<uint32_t>& j) {
+    std::vector<uint32_t> rooted(N, 0), off(N, 0);
+    slot.assign(F, 0);
+    j.assign(F, 0);
+    for (uint32_t f = 0; f < F; ++f) j[f] = rooted[trt_frame_root(first + f, N, root)]++;
+    for (uint32_t r = 1; r < N; ++r) off[r] = off[r - 1] + rooted[r - 1];
+    for (uint32_t f = 0; f < F; ++f) slot[f] = off[trt_frame_root(first + f, N, root)] + j[f];
 }
 
 } // namespace trt

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/trt/abi.h"
@@ -408,6 +409,86 @@ bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out)
         q.pad[0] = q.pad[1] = 0;
         for (int i = 0; i < 4; ++i) q.child[i] = nd.child[i];
     }
+    return true;
+}
+
+// The 48-B form of the quantized nodes (trt_device.h Bvh4CNode).  Checks that every node's
+// inner children are consecutive nodes (collapse_bvh4 numbers them so), then reorders the leaf
+// triangle array node by node — each node's leaf children in slot order, so they are
+// consecutive — and remaps the leaf references of the BVH2 and BVH4 (whose walks read the same
+// array).  Returns false (nothing changed) when a node cannot be expressed: >= 2^20 nodes, a
+// leaf of more than 8 triangles, or non-consecutive inner children.
+bool compress_bvh4(std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4, const std::vector<Bvh4QNode>& q,
+                   std::vector<TriGeo>& leaf_tris, std::vector<Bvh4CNode>& out) {
+    if (b4.empty() || b4.size() != q.size() || b4.size() >= kBvh4cMaxNodes) return false;
+    auto leaf_count = [](uint32_t r) { return ((r >> kBvhCountShift) & 15u) + 1u; };
+    std::vector<TriGeo> tris2;
+    tris2.reserve(leaf_tris.size());
+    std::unordered_map<uint32_t, uint32_t> first_map; // old leaf first -> new first
+    std::vector<Bvh4CNode> c(b4.size());
+    for (size_t n = 0; n < b4.size(); ++n) {
+        const Bvh4Node& nd = b4[n];
+        uint32_t base = 0, k_inner = 0, meta = 0;
+        const uint32_t tri_base = (uint32_t)tris2.size();
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t r = nd.child[i];
+            uint32_t m = 0;
+            if (r == kBvh4None) {
+                m = 0;
+            } else if (!(r & kBvhLeafBit)) {
+                if (k_inner == 0) base = r;
+                if (r != base + k_inner || r >= kBvh4cMaxNodes) return false;
+                ++k_inner;
+                m = 1;
+            } else {
+                const uint32_t cnt = leaf_count(r), first = r & kBvhFirstMask;
+                if (cnt > kBvh4cMaxLeaf || first + cnt > leaf_tris.size()) return false;
+                first_map[first] = (uint32_t)tris2.size();
+                tris2.insert(tris2.end(), leaf_tris.begin() + first, leaf_tris.begin() + first + cnt);
+                m = 2u | ((cnt - 1u) << 2);
+            }
+            meta |= m << (5 * i);
+        }
+        Bvh4CNode& o = c[n];
+        const Bvh4QNode& qq = q[n];
+        for (int a = 0; a < 3; ++a) {
+            o.p[a] = qq.p[a];
+            o.qlo[a] = qq.qlo[a];
+            o.qhi[a] = qq.qhi[a];
+        }
+        o.exps_meta = (qq.exps & 0xFFFFFFu) | ((meta & 0xFFu) << 24);
+        o.base_meta = (base & 0xFFFFFu) | ((meta >> 8) << 20);
+        o.tri_base = tri_base;
+    }
+    if (tris2.size() != leaf_tris.size()) return false; // every triangle sits in exactly one leaf
+    auto remap = [&](uint32_t r) {
+        if (r == kBvh4None || !(r & kBvhLeafBit)) return r;
+        const auto it = first_map.find(r & kBvhFirstMask);
+        return it == first_map.end() ? r : ((r & ~kBvhFirstMask) | it->second);
+    };
+    // self-check: the kernel's decode of every node gives the remapped references slot by slot,
+    // and every leaf holds the same triangles as before
+    for (size_t n = 0; n < b4.size(); ++n) {
+        const uint4 ch = bvh4c_children(c[n].exps_meta, c[n].base_meta, c[n].tri_base);
+        const uint32_t got[4] = {ch.x, ch.y, ch.z, ch.w};
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t old_r = b4[n].child[i], want = remap(old_r);
+            if (got[i] != want) return false;
+            if (want != kBvh4None && (want & kBvhLeafBit)) {
+                const uint32_t cnt = leaf_count(want);
+                for (uint32_t k = 0; k < cnt; ++k)
+                    if (std::memcmp(&tris2[(want & kBvhFirstMask) + k], &leaf_tris[(old_r & kBvhFirstMask) + k],
+                                    sizeof(TriGeo)) != 0)
+                        return false;
+            }
+        }
+    }
+    for (auto& nd : b4)
+        for (auto& r : nd.child) r = remap(r);
+    for (auto& nd : b2)
+        for (auto& r : nd.child) r = remap(r);
+    leaf_tris.swap(tris2);
+    out.swap(c);
     return true;
 }
 

@@ -25,6 +25,7 @@ struct trt_ctx {
     trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
     trt::Bvh4Node* d_bvh4 = nullptr; // the same, 4-wide
     trt::Bvh4QNode* d_bvh4q = nullptr; // the same, 4-wide with quantized child boxes
+    trt::Bvh4CNode* d_bvh4c = nullptr; // the same in 48 B (implicit children)
     trt::TriGeo* d_bvh_tris = nullptr;
     uint32_t node_off[11] = {0};
     uint32_t top = 0;
@@ -92,7 +93,7 @@ struct trt_ctx {
     hipEvent_t fork_ev = nullptr;
     uint32_t fev_frames = 0;
     // bytes of each scene binding on the device (trt::kSceneBuf* order), for the broadcast
-    size_t scene_bytes[10] = {0};
+    size_t scene_bytes[11] = {0};
     void* diag = nullptr; // diagnostic builds: ray-dump buffer (trt_diag_set_buffer)
 };
 
@@ -121,8 +122,9 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
 // The scene bindings of a context in a fixed order (the RCCL scene broadcast walks them).
 enum SceneBuf : int {
     kSceneBatches = 0, kSceneNodes, kSceneBvh, kSceneBvh4, kSceneBvhTris, kSceneGeo, kSceneShade,
-    kSceneMats, kSceneEnv, kSceneBvh4Q, kSceneBufs
+    kSceneMats, kSceneEnv, kSceneBvh4Q, kSceneBvh4C, kSceneBufs
 };
+static_assert(kSceneBufs == sizeof(trt_ctx::scene_bytes) / sizeof(size_t), "one byte count per scene binding");
 void** scene_buf(trt_ctx* c, int k);
 
 // Everything besides the device buffers that trt_upload_scene derives (fixed size, broadcast

@@ -92,6 +92,43 @@ struct alignas(16) Bvh4QNode {
 };
 static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode is 64 B");
 
+// The quantized node in 48 B (3 x dwordx4 per visit instead of 4): the child references are
+// implicit.  A node's inner children are consecutive nodes from `base` on (collapse_bvh4's BFS
+// numbering), and its leaf children's triangles are consecutive from `tri_base` on (the leaf
+// triangle array is reordered node by node, compress_bvh4).  Per slot i, 5 bits of `meta`
+// (bits 5i .. 5i+4): kind (0 unused, 1 inner, 2 leaf) | (leaf triangles - 1) << 2.  The 20
+// meta bits ride in the spare top byte of the exponent word (bits 0-7) and above a 20-bit
+// `base` (bits 8-19).  Same boxes as Bvh4QNode (bit-identical planes), same node indices.
+constexpr uint32_t kBvh4cMaxNodes = 1u << 20;
+constexpr uint32_t kBvh4cMaxLeaf = 8u;
+struct alignas(16) Bvh4CNode {
+    float p[3];
+    uint32_t exps_meta;  // e_x | e_y << 8 | e_z << 16 | meta[0:8] << 24
+    uint32_t qlo[3];
+    uint32_t qhi[3];
+    uint32_t base_meta;  // first inner child (20 bits) | meta[8:20] << 20
+    uint32_t tri_base;   // first triangle of the leaf children
+};
+static_assert(sizeof(Bvh4CNode) == 48, "Bvh4CNode is 3 x dwordx4");
+
+// Child references of a 48-B node (kBvh4None, an inner node index, or a leaf reference as in
+// BvhNode): inner children consecutive from base, leaf children's triangles consecutive from
+// tri_base, in slot order.  Shared by the kernel's walk and the builder's self-check.
+__host__ __device__ inline uint4 bvh4c_children(uint32_t exps_meta, uint32_t base_meta, uint32_t tri_base) {
+    const uint32_t meta = (exps_meta >> 24) | ((base_meta >> 20) << 8);
+    uint32_t nb = base_meta & 0xFFFFFu, tb = tri_base;
+    uint32_t r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t m = (meta >> (5 * i)) & 31u;
+        const uint32_t kind = m & 3u, cm1 = m >> 2;
+        r[i] = kind == 1u ? nb : kind == 2u ? (kBvhLeafBit | (cm1 << kBvhCountShift) | tb) : kBvh4None;
+        nb += kind == 1u ? 1u : 0u;
+        tb += kind == 2u ? cm1 + 1u : 0u;
+    }
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
 struct Mat {
     float albedo[4];
     float kd[3];
@@ -195,6 +232,7 @@ struct KArgs {
     const BvhNode* __restrict__ bvh;  // per-lane BVH over triangles, or null (batch walk)
     const Bvh4Node* __restrict__ bvh4; // the same BVH collapsed to 4-wide nodes
     const Bvh4QNode* __restrict__ bvh4q; // ... with quantized child boxes (same node indices)
+    const Bvh4CNode* __restrict__ bvh4c; // ... quantized, implicit children, 48 B (used when set)
     const TriGeo* __restrict__ bvh_tris; // BVH-ordered geometry; pad = (triangle, batch, ni)
     const float4* __restrict__ nodes; // batch hierarchy: per node (lo.xyz, -), (hi.xyz, -)
     uint32_t node_off[11];            // first node of level L (L = 1..top) in `nodes`

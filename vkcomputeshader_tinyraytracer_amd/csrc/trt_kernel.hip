@@ -669,12 +669,79 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 #ifndef TRT_ROOT_SCALAR
 #define TRT_ROOT_SCALAR 1
 #endif
+// Wave-uniform node fetch: when every lane at an internal node visits the same node, one scalar
+// fetch replaces the per-lane loads (C4 -4 %, C3 -1 %, shipped frame -3 %: the walk is bound by
+// the vector-memory pipe, TA/TD, not by bytes; profiles/r03_ab_c4_walk.log).
+#ifndef TRT_UNIFORM_NODE
+#define TRT_UNIFORM_NODE 1
+#endif
+// 48-B nodes with implicit children (trt_device.h Bvh4CNode): measured slower than the 64-B
+// quantized nodes on C4 (+5 %) and neutral elsewhere (profiles/r03_ab_c4_walk.log), so the walk
+// is compiled only on request (-DTRT_BVH_COMPRESS=1, with TRT_BVH_COMPRESS=1 at upload).
+#ifndef TRT_BVH_COMPRESS
+#define TRT_BVH_COMPRESS 0
+#endif
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
     BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2> stack(slab);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
+#if TRT_BVH_COMPRESS
+    // 48-B quantized nodes (3 x dwordx4 per visit): the walk of the quantized nodes below with
+    // the child references rebuilt from the node's implicit layout (the host sets bvh4c only for
+    // the builds it measured faster with them)
+    if (A.bvh4c) {
+        {
+            typedef __attribute__((address_space(4))) const float cfloat;
+            typedef __attribute__((address_space(4))) const uint32_t cuint;
+            const cfloat* R = (const cfloat*)(A.bvh4c);
+            const cuint* RC = (const cuint*)(A.bvh4c);
+            const float4 pe = make_float4(R[0], R[1], R[2], R[3]);
+            const uint4 qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+            const uint4 qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+#ifdef TRT_DIAG_PIXEL_WORK
+            ++c.wn;
+#endif
+            if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, bvh4c_children(RC[3], RC[10], RC[11]), stack, node, c))
+                return;
+        }
+        for (;;) {
+            if (!(node & kBvhLeafBit)) {
+                float4 pe;
+                uint4 qa, qb;
+#if TRT_UNIFORM_NODE
+                const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
+                if (__ballot(node != n0) == 0ull) {
+                    typedef __attribute__((address_space(4))) const float cfloat;
+                    typedef __attribute__((address_space(4))) const uint32_t cuint;
+                    const cfloat* R = (const cfloat*)(A.bvh4c + n0);
+                    const cuint* RC = (const cuint*)(A.bvh4c + n0);
+                    pe = make_float4(R[0], R[1], R[2], R[3]);
+                    qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+                    qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+                } else
+#endif
+                {
+                    const float4* p = reinterpret_cast<const float4*>(A.bvh4c + node);
+                    pe = p[0];
+                    qa = reinterpret_cast<const uint4*>(p)[1];
+                    qb = reinterpret_cast<const uint4*>(p)[2];
+                }
+#ifdef TRT_DIAG_PIXEL_WORK
+                ++c.wn;
+#endif
+                const uint4 ch = bvh4c_children(__float_as_uint(pe.w), qb.z, qb.w);
+                if (visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) continue;
+            } else if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
+                occluded = true;
+                return;
+            }
+            if (stack.sp == 0) return;
+            node = stack.pop();
+        }
+    }
+#endif
 #if TRT_BVH_QUANT
     // measured: -3 % on C4 (1,600 batches, 4-wave build), +2..3 % on C3 / the shipped frame
     // (profiles/r02_ab_quant.log), so the quantized nodes serve the 4-wave build only
@@ -695,11 +762,30 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
         }
         for (;;) {
             if (!(node & kBvhLeafBit)) {
-                const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
-                const float4 pe = p[0];
-                const uint4 qa = reinterpret_cast<const uint4*>(p)[1];
-                const uint4 qb = reinterpret_cast<const uint4*>(p)[2];
-                const uint4 ch = reinterpret_cast<const uint4*>(p)[3];
+                float4 pe;
+                uint4 qa, qb, ch;
+#if TRT_UNIFORM_NODE
+                // every lane at an internal node visits the same node (coherent rays, top levels):
+                // one scalar fetch for the wave instead of 4 per-lane dwordx4 loads through TA/TD
+                const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
+                if (__ballot(node != n0) == 0ull) {
+                    typedef __attribute__((address_space(4))) const float cfloat;
+                    typedef __attribute__((address_space(4))) const uint32_t cuint;
+                    const cfloat* R = (const cfloat*)(A.bvh4q + n0);
+                    const cuint* RC = (const cuint*)(A.bvh4q + n0);
+                    pe = make_float4(R[0], R[1], R[2], R[3]);
+                    qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+                    qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+                    ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
+                } else
+#endif
+                {
+                    const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
+                    pe = p[0];
+                    qa = reinterpret_cast<const uint4*>(p)[1];
+                    qb = reinterpret_cast<const uint4*>(p)[2];
+                    ch = reinterpret_cast<const uint4*>(p)[3];
+                }
 #ifdef TRT_DIAG_PIXEL_WORK
                 ++c.wn;
 #endif
@@ -736,9 +822,29 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 #endif
     for (;;) {
         if (!(node & kBvhLeafBit)) {
-            const float4* p = reinterpret_cast<const float4*>(A.bvh4 + node);
-            const float4 lx = p[0], ly = p[1], lz = p[2], hx = p[3], hy = p[4], hz = p[5];
-            const uint4 ch = reinterpret_cast<const uint4*>(p)[6];
+            float4 lx, ly, lz, hx, hy, hz;
+            uint4 ch;
+#if TRT_UNIFORM_NODE
+            const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
+            if (__ballot(node != n0) == 0ull) { // one scalar fetch for the wave (see visit4q's loop)
+                typedef __attribute__((address_space(4))) const float cfloat;
+                typedef __attribute__((address_space(4))) const uint32_t cuint;
+                const cfloat* R = (const cfloat*)(A.bvh4 + n0);
+                const cuint* RC = (const cuint*)(A.bvh4 + n0);
+                lx = make_float4(R[0], R[1], R[2], R[3]);
+                ly = make_float4(R[4], R[5], R[6], R[7]);
+                lz = make_float4(R[8], R[9], R[10], R[11]);
+                hx = make_float4(R[12], R[13], R[14], R[15]);
+                hy = make_float4(R[16], R[17], R[18], R[19]);
+                hz = make_float4(R[20], R[21], R[22], R[23]);
+                ch = make_uint4(RC[24], RC[25], RC[26], RC[27]);
+            } else
+#endif
+            {
+                const float4* p = reinterpret_cast<const float4*>(A.bvh4 + node);
+                lx = p[0], ly = p[1], lz = p[2], hx = p[3], hy = p[4], hz = p[5];
+                ch = reinterpret_cast<const uint4*>(p)[6];
+            }
 #ifdef TRT_DIAG_PIXEL_WORK
             ++c.wn;
 #endif
@@ -2080,21 +2186,24 @@ hipError_t launch_envp(const uint32_t* env, uint2* out, uint32_t W, uint32_t H, 
 
 // ---- multi-GPU frame assembly (trt_multi.cpp) ----------------------------------------------
 //
-// Re-interleaves the compact band-group buffers a gather delivered to the root: output row y
-// of frame f belongs to band b = y / B, band group g = b % NG, compact row k = (b / NG) * B +
-// y % B (the inverse of band_row above), stored at gather + ((f * NG + g) * max_rows + k) * W.
-// One 256-thread workgroup per output row; rows are copied as 16-byte vectors when aligned.
+// Re-interleaves the compact band-group buffers an exchange delivered to a root (the layout of
+// band_plan.cpp / abi.h trt_band_plan): output row y of the root's frame f (0..J-1) belongs to
+// band b = y / B, band group g = b % NG, compact row k = (b / NG) * B + y % B (trt_bands.h, the
+// inverse of band_row above); group g = q * G + v of sender q sits at gather + (((q * J + f) *
+// G + v) * max_rows + k) * W.  One 256-thread workgroup per output row; rows are copied as
+// 16-byte vectors when aligned.
 namespace trt {
 
 __global__ __launch_bounds__(256) void interleave_kernel(const uint32_t* __restrict__ gather, uint32_t* __restrict__ out,
-                                                         uint32_t W, uint32_t H, uint32_t B, uint32_t NG,
-                                                         uint32_t max_rows, size_t stride_px, int vec4,
+                                                         uint32_t W, uint32_t H, uint32_t B, uint32_t NG, uint32_t G,
+                                                         uint32_t J, uint32_t max_rows, size_t stride_px, int vec4,
                                                          uint32_t skip_lo, uint32_t skip_hi) {
     const uint32_t f = blockIdx.x / H, y = blockIdx.x % H;
     uint32_t g, k;
     band_of_row(y, B, NG, g, k); // trt_bands.h
     if (g >= skip_lo && g < skip_hi) return; // the root's own groups, rendered in place
-    const uint32_t* src = gather + ((size_t)(f * NG + g) * max_rows + k) * W;
+    const uint32_t q = g / G, v = g % G;
+    const uint32_t* src = gather + ((size_t)((q * J + f) * G + v) * max_rows + k) * W;
     uint32_t* dst = out + (size_t)f * stride_px + (size_t)y * W;
     if (vec4) {
         const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -2106,14 +2215,15 @@ __global__ __launch_bounds__(256) void interleave_kernel(const uint32_t* __restr
 }
 
 hipError_t launch_interleave(const uint32_t* gather, uint32_t* out, uint32_t width, uint32_t height,
-                             uint32_t band_rows, uint32_t groups, uint32_t max_rows, uint32_t nframes,
-                             size_t frame_stride_px, hipStream_t stream, uint32_t skip_lo, uint32_t skip_hi) {
+                             uint32_t band_rows, uint32_t groups, uint32_t groups_per_rank, uint32_t max_rows,
+                             uint32_t nframes, size_t frame_stride_px, hipStream_t stream, uint32_t skip_lo,
+                             uint32_t skip_hi) {
     if (skip_lo == 0 && skip_hi >= groups) return hipSuccess; // every group was rendered in place
-    if (!width || !height || !nframes) return hipSuccess;
+    if (!width || !height || !nframes || !groups_per_rank) return hipSuccess;
     const int vec4 = (width % 4u == 0u) && ((reinterpret_cast<uintptr_t>(out) & 15u) == 0u) &&
                      (frame_stride_px % 4u == 0u) && ((reinterpret_cast<uintptr_t>(gather) & 15u) == 0u);
     hipLaunchKernelGGL(interleave_kernel, dim3(height * nframes), dim3(256), 0, stream, gather, out, width, height,
-                       band_rows, groups, max_rows, frame_stride_px, vec4, skip_lo, skip_hi);
+                       band_rows, groups, groups_per_rank, nframes, max_rows, frame_stride_px, vec4, skip_lo, skip_hi);
     return hipGetLastError();
 }
 

@@ -41,8 +41,9 @@
 
 namespace trt {
 hipError_t launch_interleave(const uint32_t* gather, uint32_t* out, uint32_t width, uint32_t height,
-                             uint32_t band_rows, uint32_t groups, uint32_t max_rows, uint32_t nframes,
-                             size_t frame_stride_px, hipStream_t stream, uint32_t skip_lo, uint32_t skip_hi);
+                             uint32_t band_rows, uint32_t groups, uint32_t groups_per_rank, uint32_t max_rows,
+                             uint32_t nframes, size_t frame_stride_px, hipStream_t stream, uint32_t skip_lo,
+                             uint32_t skip_hi);
 }
 
 struct trt_multi {
@@ -314,8 +315,9 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         if (rc != TRT_OK) return rc;
         if (total) return mfail(m, TRT_ERR_OOM, why.empty() ? "a peer rank failed to allocate its batch buffers" : why);
     }
-    std::vector<uint32_t> froot(nf);
+    std::vector<uint32_t> froot(nf), fslot, fj;
     for (uint32_t f = 0; f < nf; ++f) froot[f] = trt_frame_root(rot0 + f, N, root);
+    trt::band_plan_slots(N, rot0, nf, root, fslot, fj);
     // render
     std::vector<trt::FrameOut> fl(nf);
     for (size_t li = 0; li < m->devs.size(); ++li) {
@@ -334,8 +336,8 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
                 const trt_ubo* u = ubos ? &ubos[f] : nullptr;
                 if (froot[f] == d.rank && !m->self_gather) // own frame: in place, never travels
                     fl[f] = trt::FrameOut{u, (out8 && out8[li]) ? out8[li] + (size_t)f * frame_stride : nullptr, true};
-                else
-                    fl[f] = trt::FrameOut{u, d.local[slot] + ((size_t)f * G + v) * blk, false};
+                else // frames ordered by root: the J blocks for one root are contiguous
+                    fl[f] = trt::FrameOut{u, d.local[slot] + ((size_t)fslot[f] * G + v) * blk, false};
             }
             const int rc = trt::render_frame_list(d.ctx, &q, fl.data(), nf, 0);
             if (rc != TRT_OK) {
@@ -347,7 +349,7 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         MHIP(m, hipEventRecord(d.rendered[slot], rs));
         MHIP(m, hipStreamWaitEvent(d.comm_stream, d.rendered[slot], 0));
     }
-    // gather: the plan's transfers, in list order on both ends (pairs match in order)
+    // gather: the plan's transfers (one per sender-root pair), in list order on both ends
     if (!plan.empty()) {
         NcclGroup grp(m);
         CNCCL(m, grp.start());
@@ -362,7 +364,8 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         }
         CNCCL(m, grp.end());
     }
-    // re-interleave: a root's frames of the batch are f0, f0 + step, ... (rotation) or all
+    // re-interleave: a root's frames of the batch are f0, f0 + step, ... (rotation) or all;
+    // sender q's blocks of its j-th frame at ((q * J + j) * G + v) * blk
     for (size_t li = 0; li < m->devs.size(); ++li) {
         auto& d = m->devs[li];
         MHIP(m, hipSetDevice(d.device));
@@ -377,7 +380,7 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
             const uint32_t lo = m->self_gather ? 0u : d.rank * G, hi = m->self_gather ? 0u : d.rank * G + G;
             MHIP(m, trt::launch_interleave(reinterpret_cast<const uint32_t*>(d.gather[slot]),
                                            reinterpret_cast<uint32_t*>(out8[li] + (size_t)f0 * frame_stride), W, H,
-                                           band_rows, NG, L.max_rows, cnt, (size_t)step * frame_stride / 4,
+                                           band_rows, NG, G, L.max_rows, cnt, (size_t)step * frame_stride / 4,
                                            d.comm_stream, lo, hi));
         }
         MHIP(m, hipEventRecord(d.gathered[slot], d.comm_stream));

@@ -39,6 +39,8 @@ hipError_t launch_envp(const uint32_t* env, uint2* out, uint32_t W, uint32_t H, 
 hipError_t launch_shadow_batch(const KArgs& A, const float4* rays, uint32_t n, uint32_t* occ, hipStream_t stream);
 uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4);
 bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out);
+bool compress_bvh4(std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4, const std::vector<Bvh4QNode>& q,
+                   std::vector<TriGeo>& leaf_tris, std::vector<Bvh4CNode>& out);
 bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris);
 }
@@ -73,6 +75,7 @@ void free_scene(trt_ctx* c) {
     (void)hipFree(c->d_bvh);
     (void)hipFree(c->d_bvh4);
     (void)hipFree(c->d_bvh4q);
+    (void)hipFree(c->d_bvh4c);
     (void)hipFree(c->d_bvh_tris);
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade);
@@ -83,6 +86,7 @@ void free_scene(trt_ctx* c) {
     c->d_bvh = nullptr;
     c->d_bvh4 = nullptr;
     c->d_bvh4q = nullptr;
+    c->d_bvh4c = nullptr;
     c->d_bvh_tris = nullptr;
     c->top = 0;
     c->d_geo = nullptr;
@@ -119,6 +123,14 @@ Mat to_mat(const trt_material& m) {
     r.spec_exp = m.diffuse_specular.w;
     r.ior = m.refractive.x;
     return r;
+}
+
+// TRT_BVH_COMPRESS: 0 = no 48-B nodes (default: measured slower), 1 = for
+// the 4-wave BVH build, 2 = every BVH4 walk; the kernel walks them only when built with
+// -DTRT_BVH_COMPRESS=1.  Read at every scene upload / frame.
+int bvh_compress_mode() {
+    const char* e = std::getenv("TRT_BVH_COMPRESS");
+    return e ? std::atoi(e) : 0;
 }
 
 void fill_ubo_args(KArgs& A, const trt_ubo& u) {
@@ -470,9 +482,20 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         if (trt::collapse_bvh4(bvh, bvh4) > (uint32_t)trt::kBvhStack) bvh4.clear();
         bvh4_n = bvh4.size();
         std::vector<trt::Bvh4QNode> bvh4q;
-        if (!bvh4.empty() && trt::quantize_bvh4(bvh4, bvh4q) &&
-            (rc = upload((void**)&c->d_bvh4q, bvh4q.data(), sizeof(trt::Bvh4QNode) * bvh4q.size(),
-                         "upload quantized bvh4")) != TRT_OK) {
+        std::vector<trt::Bvh4CNode> bvh4c;
+        const bool quant = !bvh4.empty() && trt::quantize_bvh4(bvh4, bvh4q);
+        // the 48-B form of the quantized nodes reorders the leaf triangles (and remaps the leaf
+        // references of every walk), so it is made before anything is uploaded
+        if (quant && bvh_compress_mode() != 0) {
+            if (!trt::compress_bvh4(bvh, bvh4, bvh4q, bvh_tris, bvh4c)) bvh4c.clear();
+        }
+        if (quant && (rc = upload((void**)&c->d_bvh4q, bvh4q.data(), sizeof(trt::Bvh4QNode) * bvh4q.size(),
+                                  "upload quantized bvh4")) != TRT_OK) {
+            free_scene(c);
+            return rc;
+        }
+        if (!bvh4c.empty() && (rc = upload((void**)&c->d_bvh4c, bvh4c.data(), sizeof(trt::Bvh4CNode) * bvh4c.size(),
+                                           "upload compressed bvh4")) != TRT_OK) {
             free_scene(c);
             return rc;
         }
@@ -506,6 +529,7 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
     }
     if (c->d_bvh4) sb[trt::kSceneBvh4] = sizeof(trt::Bvh4Node) * bvh4_n;
     if (c->d_bvh4q) sb[trt::kSceneBvh4Q] = sizeof(trt::Bvh4QNode) * bvh4_n;
+    if (c->d_bvh4c) sb[trt::kSceneBvh4C] = sizeof(trt::Bvh4CNode) * bvh4_n;
     if (c->d_env) sb[trt::kSceneEnv] = (size_t)env_w * env_h * 4;
     c->nbatch = nmodel;
     c->top = top;
@@ -604,6 +628,9 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // (1,600 batches), +1 % on C3 and the shipped frame (80 / 594 batches), so large scenes only
     // (profiles/r01_ab_occupancy.log).
     A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : (c->nbatch >= 1024u ? 1u : 0u);
+    // 48-B nodes: for the 4-wave build (mode 1, the default), or for every BVH4 walk (mode 2)
+    const int cm = bvh_compress_mode();
+    A.bvh4c = (c->d_bvh4c && (cm == 2 || (cm == 1 && A.bvh_waves4))) ? c->d_bvh4c : nullptr;
 }
 
 // Does this frame run deferred shadows?  Auto: mesh scenes with max_depth >= 8, whose deep
@@ -1103,6 +1130,7 @@ void** scene_buf(trt_ctx* c, int k) {
     case kSceneShade: return reinterpret_cast<void**>(&c->d_shade);
     case kSceneMats: return reinterpret_cast<void**>(&c->d_mats);
     case kSceneBvh4Q: return reinterpret_cast<void**>(&c->d_bvh4q);
+    case kSceneBvh4C: return reinterpret_cast<void**>(&c->d_bvh4c);
     default: return reinterpret_cast<void**>(&c->d_env);
     }
 }
@@ -1187,5 +1215,29 @@ extern "C" int trt_diag_shadow_batch(trt_ctx* c, const trt_params* p, const void
     KArgs A;
     fill_args(c, p, A);
     HIP_TRY(c, trt::launch_shadow_batch(A, static_cast<const float4*>(rays), n, static_cast<uint32_t*>(occ), c->stream));
+    return TRT_OK;
+}
+
+// Host-only check of the BVH pipeline of trt_upload_scene (no GPU): BVH2 build, 4-wide
+// collapse, quantization and the 48-B compression with its self-check.  out[0] BVH2 nodes,
+// out[1] BVH4 nodes, out[2] quantized (0/1), out[3] compressed (0/1), out[4] worst-case BVH4
+// stack, out[5] leaf triangles.  Returns TRT_ERR_INVALID when no BVH is built (overlapping
+// batch ranges).
+extern "C" int trt_diag_bvh_build(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
+                                  uint64_t out[6]) {
+    if (!out || (ntri && !tris) || (nmodel && !models)) return TRT_ERR_INVALID;
+    for (int i = 0; i < 6; ++i) out[i] = 0;
+    std::vector<trt::BvhNode> bvh;
+    std::vector<TriGeo> bvh_tris;
+    if (!nmodel || !trt::build_bvh(tris, ntri, models, nmodel, bvh, bvh_tris)) return TRT_ERR_INVALID;
+    std::vector<trt::Bvh4Node> bvh4;
+    out[0] = bvh.size();
+    out[4] = trt::collapse_bvh4(bvh, bvh4);
+    out[1] = bvh4.size();
+    std::vector<trt::Bvh4QNode> q;
+    std::vector<trt::Bvh4CNode> cn;
+    out[2] = (!bvh4.empty() && trt::quantize_bvh4(bvh4, q)) ? 1 : 0;
+    out[3] = (out[2] && trt::compress_bvh4(bvh, bvh4, q, bvh_tris, cn)) ? 1 : 0;
+    out[5] = bvh_tris.size();
     return TRT_OK;
 }

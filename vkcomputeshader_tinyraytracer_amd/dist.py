@@ -63,51 +63,54 @@ class TiledFrames:
         N, G, r = self.world, self.G, self.rank
         lay, plan = band_plan(W, H, self.band_rows, N, G, first_frame, nframes, self.root, self_gather=True)
         NG, blk = lay.groups, lay.block_bytes
+        # the plan's buffer layout (abi.h trt_band_plan): batch frames ordered by root
+        roots = [frame_root(first_frame + f, N, self.root) for f in range(nframes)]
+        J = [roots.count(q) for q in range(N)]
+        off = [sum(J[:q]) for q in range(N)]
+        jth = [roots[:f].count(roots[f]) for f in range(nframes)]
         local = torch.zeros(max(lay.local_bytes, 1), dtype=torch.uint8, device=self.device)
-        gather = torch.zeros(max(nframes * NG * blk, 1), dtype=torch.uint8, device=self.device)
-        # 1. this rank's band groups of every frame, compactly at (f * G + v) * blk
+        gather = torch.zeros(max(lay.gather_bytes, 1), dtype=torch.uint8, device=self.device)
+        # 1. this rank's band groups of every frame, compactly at ((off_root + j) * G + v) * blk
         for f in range(nframes):
             for v in range(G):
                 g = r * G + v
                 q = band_params(self.params, self.band_rows, NG, g)
                 rows = len(T.output_rows(H, q.band_rows, q.band_count, q.band_index))
                 if rows:
-                    off = (f * G + v) * blk
-                    render_fn(first_frame + f, g, q, local[off:off + rows * W * 4].view(rows, W, 4))
-        # 2. the plan's transfers (a rank's own groups are a local copy: torch.distributed has
-        #    no send-to-self); tags make the pairing explicit for backends that match by tag
+                    o = ((off[roots[f]] + jth[f]) * G + v) * blk
+                    render_fn(first_frame + f, g, q, local[o:o + rows * W * 4].view(rows, W, 4))
+        # 2. the plan's transfers, one per (sender, root) (a rank's own blocks are a local copy:
+        #    torch.distributed has no send-to-self)
         reqs = []
         for x in plan:
-            tag = x.frame * NG + x.group
+            src = local[x.src_offset:x.src_offset + x.bytes]
             if x.src == r and x.dst == r:
-                gather[x.dst_offset:x.dst_offset + x.bytes].copy_(local[x.src_offset:x.src_offset + x.bytes])
+                gather[x.dst_offset:x.dst_offset + x.bytes].copy_(src)
             elif x.src == r:
-                reqs.append(dist.isend(local[x.src_offset:x.src_offset + x.bytes].contiguous(), x.dst,
-                                       group=self.group, tag=tag))
+                reqs.append(dist.isend(src.contiguous(), x.dst, group=self.group, tag=x.dst))
             elif x.dst == r:
-                reqs.append(dist.irecv(gather[x.dst_offset:x.dst_offset + x.bytes], x.src, group=self.group, tag=tag))
+                reqs.append(dist.irecv(gather[x.dst_offset:x.dst_offset + x.bytes], x.src, group=self.group, tag=x.dst))
         for q in reqs:
             q.wait()
-        # 3. re-interleave the frames this rank roots (slot j of the gather buffer)
+        # 3. re-interleave the frames this rank roots: sender q's group v of the j-th frame at
+        #    ((q * J + j) * G + v) * blk
         out: dict[int, torch.Tensor] = {}
-        slot = 0
         for f in range(nframes):
-            i = first_frame + f
-            if frame_root(i, N, self.root) != r:
+            if roots[f] != r:
                 continue
+            j = jth[f]
             frame = torch.empty((H, W, 4), dtype=torch.uint8, device=self.device)
             for g in range(NG):
                 q = band_params(self.params, self.band_rows, NG, g)
                 rows = len(T.output_rows(H, q.band_rows, q.band_count, q.band_index))
                 if not rows:
                     continue
-                off = (slot * NG + g) * blk
-                src = gather[off:off + rows * W * 4].view(rows, W, 4)
+                o = (((g // G) * J[r] + j) * G + g % G) * blk
+                src = gather[o:o + rows * W * 4].view(rows, W, 4)
                 idx = torch.tensor([band_frame_row(k, self.band_rows, NG, g) for k in range(rows)],
                                    dtype=torch.long, device=self.device)
                 frame.index_copy_(0, idx, src)
-            out[i] = frame
-            slot += 1
+            out[first_frame + f] = frame
         return out
 
 

@@ -149,15 +149,15 @@ class BandLayout(ctypes.Structure):
 
 
 class BandXfer(ctypes.Structure):
-    """trt_band_xfer (abi.h): one compact band buffer travelling to a frame's root."""
+    """trt_band_xfer (abi.h): the compact band blocks one rank sends to one root."""
 
     _fields_ = [
-        ("frame", ctypes.c_uint32),
-        ("group", ctypes.c_uint32),
         ("src", ctypes.c_uint32),
         ("dst", ctypes.c_uint32),
-        ("rows", ctypes.c_uint32),
-        ("slot", ctypes.c_uint32),
+        ("frames", ctypes.c_uint32),
+        ("groups", ctypes.c_uint32),
+        ("first_slot", ctypes.c_uint32),
+        ("pad", ctypes.c_uint32),
         ("src_offset", ctypes.c_uint64),
         ("dst_offset", ctypes.c_uint64),
         ("bytes", ctypes.c_uint64),
