@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--split", type=int, default=0, help="subtree split window (0 auto, 1 off, 2..5)")
     ap.add_argument("--defer", type=int, default=0, help="deferred shadows (0 auto, 1 off, 2 on)")
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=None, help="override trt_params.flags")
+    ap.add_argument("--frame-batch", type=int, default=0, help="frames per launch (0 auto, 1 = one per frame)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -59,6 +60,7 @@ def main():
     r.set_frames_in_flight(a.inflight)
     r.set_subtree_split(a.split)
     r.set_deferred_shadows(a.defer)
+    r.set_frame_batch(a.frame_batch)
     r.render_frames(p, out, 5)
     nt = r.render_frames(p, out, a.frames, timing=True)
     ms = r.frame_times(nt)  # per frame of each launch

@@ -359,13 +359,26 @@ constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS :
 // PUSH3: the branch-free push of up to three children (push_sorted) — used by the 3-wave
 // build: C3 -4 %, shipped frame -6 %; the 4-wave build (128-VGPR cap) is 3 % slower with it
 // (profiles/r01_ab_push3.log).
+// The private tail lives in a separate array of the caller (Mem): a stack object holding the
+// dynamically indexed array AND its top index was one scratch allocation, so `sp` itself was
+// kept in scratch memory and every push / pop paid a scratch load + store of it (seen in the
+// ISA: scratch_load_dword ... offset:200 on every visit).  With the array apart, the stack
+// object is scalarised and sp lives in a register.
+// The LDS column is an address-space-3 pointer: with a generic one the compiler turned the pop's
+// `sp < N ? lds[..] : priv[..]` into one load through a selected generic pointer, i.e. a
+// flat_load that goes through the vector-memory pipe (TA/TD) even for LDS entries.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) float lds_f32;
 template <int N, bool PUSH3 = false>
 struct BvhStack {
-    uint32_t* lds; // this lane's column
-    uint32_t priv[kBvhStack - N];
+    struct Mem {
+        uint32_t priv[kBvhStack - N];
+    };
+    lds_u32* lds;   // this lane's column
+    uint32_t* priv; // the caller's private tail (scratch)
     int sp = 0;
-    __device__ __forceinline__ explicit BvhStack(float4* slab)
-        : lds(reinterpret_cast<uint32_t*>(slab) + lane_id()) {}
+    __device__ __forceinline__ BvhStack(float4* slab, Mem& m)
+        : lds((lds_u32*)(reinterpret_cast<uint32_t*>(slab) + lane_id())), priv(m.priv) {}
     __device__ __forceinline__ void push(uint32_t v) {
         if (sp < N) lds[sp * 64] = v;
         else priv[sp - N] = v;
@@ -373,7 +386,10 @@ struct BvhStack {
     }
     __device__ __forceinline__ uint32_t pop() {
         --sp;
-        return sp < N ? lds[sp * 64] : priv[sp - N];
+        uint32_t v;
+        if (sp < N) v = lds[sp * 64];
+        else v = priv[sp - N];
+        return v;
     }
     // Pushes r[nh-1], ..., r[1] (r[1] ends on top), nh in 1..4.  While three more entries fit
     // the LDS part, the three stores are unconditional: an unused one goes to slot sp + 3,
@@ -397,7 +413,9 @@ struct BvhStack {
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                           float max_dist, Cnt& c, float4* slab) {
-    BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2> stack(slab);
+    using Stack = BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2>;
+    typename Stack::Mem stack_mem;
+    Stack stack(slab, stack_mem);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
 #ifdef TRT_DIAG_PIXEL_WORK
@@ -684,7 +702,9 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
-    BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2> stack(slab);
+    using Stack = BvhStack<bvh_lds_entries<GEOM>(), GEOM == 2>;
+    typename Stack::Mem stack_mem;
+    Stack stack(slab, stack_mem);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
 #if TRT_BVH_COMPRESS
@@ -1092,7 +1112,7 @@ constexpr int lds_stack_floats() { return (CAP >= 1 && CAP <= LDS_STACK_MAX) ? C
 template <int CAP, bool LDS = (CAP <= LDS_STACK_MAX)>
 struct DeferStack;
 
-__device__ __forceinline__ void lds_put(float* p, const Seg& x) {
+__device__ __forceinline__ void lds_put(lds_f32* p, const Seg& x) {
     p[0] = x.o.x;
     p[64] = x.o.y;
     p[128] = x.o.z;
@@ -1102,15 +1122,17 @@ __device__ __forceinline__ void lds_put(float* p, const Seg& x) {
     p[384] = x.thr;
     p[448] = __int_as_float(x.depth);
 }
-__device__ __forceinline__ Seg lds_get(const float* p) {
+__device__ __forceinline__ Seg lds_get(const lds_f32* p) {
     return Seg{mk(p[0], p[64], p[128]), mk(p[192], p[256], p[320]), p[384], __float_as_int(p[448])};
 }
 
+// As BvhStack: the private entries live in the caller's Mem, so `n` stays in a register.
 template <int CAP>
 struct DeferStack<CAP, true> {
-    float* base; // this lane's column: base[(e * 8 + f) * 64]
+    struct Mem {};
+    lds_f32* base; // this lane's column: base[(e * 8 + f) * 64]
     int n = 0;
-    __device__ __forceinline__ explicit DeferStack(float* lds) : base(lds + lane_id()) {}
+    __device__ __forceinline__ DeferStack(float* lds, Mem&) : base((lds_f32*)(lds + lane_id())) {}
     __device__ __forceinline__ void push(const Seg& x) {
         lds_put(base + n * 8 * 64, x);
         ++n;
@@ -1123,9 +1145,12 @@ struct DeferStack<CAP, true> {
 
 template <int CAP>
 struct DeferStack<CAP, false> {
-    Seg s[CAP];
+    struct Mem {
+        Seg s[CAP];
+    };
+    Seg* s;
     int n = 0;
-    __device__ __forceinline__ explicit DeferStack(float*) {}
+    __device__ __forceinline__ DeferStack(float*, Mem& m) : s(m.s) {}
     __device__ __forceinline__ void push(const Seg& x) { s[n++] = x; }
     __device__ __forceinline__ Seg pop() { return s[--n]; }
 };
@@ -1133,10 +1158,13 @@ struct DeferStack<CAP, false> {
 // CL entries in LDS, then CP private ones.
 template <int CL, int CP>
 struct HybridStack {
-    float* base;
-    Seg s[CP];
+    struct Mem {
+        Seg s[CP];
+    };
+    lds_f32* base;
+    Seg* s;
     int n = 0;
-    __device__ __forceinline__ explicit HybridStack(float* lds) : base(lds + lane_id()) {}
+    __device__ __forceinline__ HybridStack(float* lds, Mem& m) : base((lds_f32*)(lds + lane_id())), s(m.s) {}
     __device__ __forceinline__ void push(const Seg& x) {
         if (n < CL) lds_put(base + n * 8 * 64, x);
         else s[n - CL] = x;
@@ -1255,7 +1283,9 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
 #endif
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    typename StackOf<CAP, HYB>::type stk(lds);
+    using Stk = typename StackOf<CAP, HYB>::type;
+    typename Stk::Mem stk_mem;
+    Stk stk(lds, stk_mem);
     for (;;) {
         uint32_t slot = 0;
         if (DEFER) {
