@@ -27,6 +27,8 @@ for v in "$@"; do
     case $v in
         base) variant base ;;
         unode) variant unode -DTRT_UNIFORM_NODE=1 ;;
+        g0w4) variant g0w4 -DTRT_G0_WAVES=1 ;;
+        g0w6) variant g0w6 -DTRT_G0_WAVES=6 ;;
         noquant) variant noquant -DTRT_BVH_QUANT=0 ;;
         noskip) variant noskip -DTRT_SKIP_DARK=0 ;;
         dumpshadow) variant dumpshadow -DTRT_DIAG_DUMP_SHADOW ;;

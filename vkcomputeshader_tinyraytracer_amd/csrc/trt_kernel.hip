@@ -1742,8 +1742,15 @@ template <int GEOM>
 constexpr int slab_float4s() {
     return GEOM == 1 ? 64 * 3 : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
 }
+// Triangle-free frames (GEOM 0: C1 / C2) are latency-bound on the dependent chain intersection
+// -> shading -> envmap gather; 5 waves per SIMD (<= 96 VGPRs) hide more of it than the 4 the
+// unconstrained build reaches (109 VGPRs): C2 15.5 -> 14.2 us per frame (round 3,
+// profiles/r03_ab_waves_c2.log; round 1 measured a 6-wave cap 20 % slower).
+#ifndef TRT_G0_WAVES
+#define TRT_G0_WAVES 5
+#endif
 template <int GEOM>
-constexpr int waves_per_simd() { return GEOM == 3 ? TRT_G3_WAVES : TRT_WAVES; }
+constexpr int waves_per_simd() { return GEOM == 3 ? TRT_G3_WAVES : GEOM == 0 ? TRT_G0_WAVES : TRT_WAVES; }
 
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
 __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_kernel(KArgs A) {

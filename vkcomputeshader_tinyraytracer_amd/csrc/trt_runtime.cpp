@@ -623,11 +623,13 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     std::memcpy(A.node_off, c->node_off, sizeof(A.node_off));
     A.ntx = (A.width + 7u) / 8u;
     A.ntiles = A.ntx * ((A.rows + 7u) / 8u);
-    // The BVH walk at 4 waves per SIMD (GEOM 3: <= 128 VGPRs, 16-entry LDS stack) hides more of
-    // the node-fetch latency of large meshes but spills a few registers: measured -13 % on C4
-    // (1,600 batches), +1 % on C3 and the shipped frame (80 / 594 batches), so large scenes only
-    // (profiles/r01_ab_occupancy.log).
-    A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : (c->nbatch >= 1024u ? 1u : 0u);
+    // The BVH walk at 4 waves per SIMD (GEOM 3: <= 128 VGPRs, 16-entry LDS stack, quantized
+    // nodes) hides more of the node-fetch latency than the 3-wave build.  Round 1 measured it
+    // for large scenes only (C4 -13 %, C3 / shipped frame +1 %, profiles/r01_ab_occupancy.log);
+    // since the traversal stack's index left scratch memory (round 3) it is ahead or equal
+    // everywhere: C4 2.90 vs 3.38 ms, C3 -9 %, shipped frame and README scene within 1 %
+    // (profiles/r03_ab_waves4_after_stack_fix.log), so it is the default for every BVH scene.
+    A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : 1u;
     // 48-B nodes: for the 4-wave build (mode 1, the default), or for every BVH4 walk (mode 2)
     const int cm = bvh_compress_mode();
     A.bvh4c = (c->d_bvh4c && (cm == 2 || (cm == 1 && A.bvh_waves4))) ? c->d_bvh4c : nullptr;
