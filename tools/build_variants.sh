@@ -28,6 +28,9 @@ for v in "$@"; do
         base) variant base ;;
         unode) variant unode -DTRT_UNIFORM_NODE=1 ;;
         g0w4) variant g0w4 -DTRT_G0_WAVES=1 ;;
+        g3lds8) variant g3lds8 -DTRT_G3_LDS=8 ;;
+        g3lds24) variant g3lds24 -DTRT_G3_LDS=24 ;;
+        g3lds12) variant g3lds12 -DTRT_G3_LDS=12 ;;
         g0w6) variant g0w6 -DTRT_G0_WAVES=6 ;;
         noquant) variant noquant -DTRT_BVH_QUANT=0 ;;
         noskip) variant noskip -DTRT_SKIP_DARK=0 ;;
