@@ -31,6 +31,15 @@ for v in "$@"; do
         g3lds8) variant g3lds8 -DTRT_G3_LDS=8 ;;
         g3lds24) variant g3lds24 -DTRT_G3_LDS=24 ;;
         g3lds12) variant g3lds12 -DTRT_G3_LDS=12 ;;
+        ww1) variant ww1 -DTRT_WHILE_WHILE=1 ;;
+        noswave) variant noswave -DTRT_SHADOW_WAVE=0 ;;
+        swe002) variant swe002 -DTRT_SHADOW_WAVE_EXT=0.02 ;;
+        swe01) variant swe01 -DTRT_SHADOW_WAVE_EXT=0.1 ;;
+        swe05) variant swe05 -DTRT_SHADOW_WAVE_EXT=0.5 ;;
+        swe007) variant swe007 -DTRT_SHADOW_WAVE_EXT=0.07 ;;
+        swe015) variant swe015 -DTRT_SHADOW_WAVE_EXT=0.15 ;;
+        swe025) variant swe025 -DTRT_SHADOW_WAVE_EXT=0.25 ;;
+        ww2) variant ww2 -DTRT_WHILE_WHILE=2 ;;
         g0w6) variant g0w6 -DTRT_G0_WAVES=6 ;;
         noquant) variant noquant -DTRT_BVH_QUANT=0 ;;
         noskip) variant noskip -DTRT_SKIP_DARK=0 ;;

@@ -39,10 +39,17 @@ def main():
     nodes, tris, segs, qmax = (w[..., k] for k in range(4))
     H, W = nodes.shape
     tiles = nodes[: H // 8 * 8, : W // 8 * 8].reshape(H // 8, 8, W // 8, 8).max(axis=(1, 3))
+    def tile_eff(a):
+        """work / (64 x the tile's busiest lane): how much of an 8x8 one-wave tile's lane time the
+        work fills if every lane walks as long as the tile's longest"""
+        t = a[: H // 8 * 8, : W // 8 * 8].reshape(H // 8, 8, W // 8, 8)
+        return float(t.sum() / max(64.0 * t.max(axis=(1, 3)).sum(), 1.0))
     order = np.argsort(nodes.ravel())[::-1][:10]
     res = {
         "config": a.config,
         "nodes_total": float(nodes.sum()), "tris_total": float(tris.sum()), "segments_total": float(segs.sum()),
+        "nodes_per_pixel": float(nodes.mean()), "tris_per_pixel": float(tris.mean()),
+        "tile_eff_nodes": tile_eff(nodes), "tile_eff_tris": tile_eff(tris), "tile_eff_work": tile_eff(nodes + tris),
         "nodes_pct": {q: float(np.percentile(nodes, q)) for q in (50, 90, 99, 99.9, 100)},
         "segs_pct": {q: float(np.percentile(segs, q)) for q in (50, 90, 99, 99.9, 100)},
         "qmax_pct": {q: float(np.percentile(qmax, q)) for q in (50, 90, 99, 99.9, 100)},

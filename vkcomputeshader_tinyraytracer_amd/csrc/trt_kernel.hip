@@ -355,6 +355,9 @@ constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 #endif
 template <int GEOM>
 constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS : 0) : kBvhLdsStack; }
+// 32-bit words of a wave's BVH-stack LDS (slab_float4s below holds them)
+template <int GEOM>
+constexpr int slab_words() { return bvh_lds_entries<GEOM>() * 64; }
 
 // PUSH3: the branch-free push of up to three children (push_sorted) — used by the 3-wave
 // build: C3 -4 %, shipped frame -6 %; the 4-wave build (128-VGPR cap) is 3 % slower with it
@@ -699,6 +702,11 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 #ifndef TRT_BVH_COMPRESS
 #define TRT_BVH_COMPRESS 0
 #endif
+// Loop shape of the quantized walk: 0 = one node or one leaf per iteration (if-if),
+// 1 = while-while, 2 = speculative while-while (leaves parked until the wave has one each).
+#ifndef TRT_WHILE_WHILE
+#define TRT_WHILE_WHILE 0
+#endif
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
@@ -780,32 +788,89 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 #endif
             if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) return;
         }
+        auto fetch = [&](uint32_t nd, float4& pe, uint4& qa, uint4& qb, uint4& ch) {
+#if TRT_UNIFORM_NODE
+            // every lane at an internal node visits the same node (coherent rays, top levels):
+            // one scalar fetch for the wave instead of 4 per-lane dwordx4 loads through TA/TD
+            const uint32_t n0 = __builtin_amdgcn_readfirstlane(nd);
+            if (__ballot(nd != n0) == 0ull) {
+                typedef __attribute__((address_space(4))) const float cfloat;
+                typedef __attribute__((address_space(4))) const uint32_t cuint;
+                const cfloat* R = (const cfloat*)(A.bvh4q + n0);
+                const cuint* RC = (const cuint*)(A.bvh4q + n0);
+                pe = make_float4(R[0], R[1], R[2], R[3]);
+                qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+                qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+                ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
+                return;
+            }
+#endif
+            const float4* p = reinterpret_cast<const float4*>(A.bvh4q + nd);
+            pe = p[0];
+            qa = reinterpret_cast<const uint4*>(p)[1];
+            qb = reinterpret_cast<const uint4*>(p)[2];
+            ch = reinterpret_cast<const uint4*>(p)[3];
+        };
+#if TRT_WHILE_WHILE == 1
+        // while-while: the wave descends inner nodes until every lane stands on a leaf (or has
+        // finished), then tests the leaves together
+        for (;;) {
+            while (!(node & kBvhLeafBit)) {
+                float4 pe;
+                uint4 qa, qb, ch;
+                fetch(node, pe, qa, qb, ch);
+#ifdef TRT_DIAG_PIXEL_WORK
+                ++c.wn;
+#endif
+                if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) {
+                    if (stack.sp == 0) return;
+                    node = stack.pop();
+                }
+            }
+            if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
+                occluded = true;
+                return;
+            }
+            if (stack.sp == 0) return;
+            node = stack.pop();
+        }
+#elif TRT_WHILE_WHILE == 2
+        // speculative while-while: a lane that reaches a leaf parks it and keeps descending
+        // until every lane still walking has parked one (or reaches a second leaf), then the
+        // parked leaves are tested together
+        for (;;) {
+            uint32_t parked = kBvh4None;
+            for (;;) {
+                if (node == kBvh4None) break;
+                if (node & kBvhLeafBit) {
+                    if (parked != kBvh4None) break;
+                    parked = node;
+                    node = stack.sp ? stack.pop() : kBvh4None;
+                } else {
+                    float4 pe;
+                    uint4 qa, qb, ch;
+                    fetch(node, pe, qa, qb, ch);
+#ifdef TRT_DIAG_PIXEL_WORK
+                    ++c.wn;
+#endif
+                    if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c))
+                        node = stack.sp ? stack.pop() : kBvh4None;
+                }
+                const bool searching = parked == kBvh4None;
+                if (__ballot(searching) == 0ull) break;
+            }
+            if (parked != kBvh4None && bvh_leaf<COUNT, SHADOW>(A, parked, o, d, inv, h, max_dist, best, c)) {
+                occluded = true;
+                return;
+            }
+            if (node == kBvh4None) return;
+        }
+#else
         for (;;) {
             if (!(node & kBvhLeafBit)) {
                 float4 pe;
                 uint4 qa, qb, ch;
-#if TRT_UNIFORM_NODE
-                // every lane at an internal node visits the same node (coherent rays, top levels):
-                // one scalar fetch for the wave instead of 4 per-lane dwordx4 loads through TA/TD
-                const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
-                if (__ballot(node != n0) == 0ull) {
-                    typedef __attribute__((address_space(4))) const float cfloat;
-                    typedef __attribute__((address_space(4))) const uint32_t cuint;
-                    const cfloat* R = (const cfloat*)(A.bvh4q + n0);
-                    const cuint* RC = (const cuint*)(A.bvh4q + n0);
-                    pe = make_float4(R[0], R[1], R[2], R[3]);
-                    qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
-                    qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
-                    ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
-                } else
-#endif
-                {
-                    const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
-                    pe = p[0];
-                    qa = reinterpret_cast<const uint4*>(p)[1];
-                    qb = reinterpret_cast<const uint4*>(p)[2];
-                    ch = reinterpret_cast<const uint4*>(p)[3];
-                }
+                fetch(node, pe, qa, qb, ch);
 #ifdef TRT_DIAG_PIXEL_WORK
                 ++c.wn;
 #endif
@@ -817,6 +882,7 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
             if (stack.sp == 0) return;
             node = stack.pop();
         }
+#endif
     }
 #endif
 #if TRT_ROOT_SCALAR
@@ -886,6 +952,133 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 // skip the mesh instead — the same (empty) result.
 __device__ __forceinline__ bool ray_misses_all_batches(f3 o, f3 d) {
     return (o.x != o.x || d.x != d.x) && (o.y != o.y || d.y != d.y) && (o.z != o.z || d.z != d.z);
+}
+
+// Wave-coherent any-hit walk of the quantized BVH4 for shadow rays.  The shading loop queries
+// one light at a time (shade loop below), so the rays a wave asks about at once share their end
+// point and, from a tile's neighbouring shading points, nearly share their origin: they visit
+// nearly the same nodes.  Here the wave walks ONE node sequence: a child is entered when any
+// lane still walking enters it, nodes and leaf triangles are read with scalar loads (one fetch
+// per wave, no per-lane vector-memory instruction at all: the per-lane walk is bound by the
+// vector-memory pipe, TA/TD), every lane tests the boxes and triangles against its own ray,
+// and a lane leaves as soon as it is occluded.  The answer is the per-lane walk's: any hit is
+// order-free, an accepted triangle is accepted on its own test (Moller-Trumbore, t < max_dist
+// and the reference's batch gate, exactly as bvh_leaf), and the union of the lanes' walks
+// contains every lane's own walk (the boxes are conservative), so no occluder is missed.
+// The walk order follows the first walking lane's entry distances.  Taken only when the
+// walking lanes' origins are within TRT_SHADOW_WAVE_EXT of the first one's: always on, the union
+// walks cost C4 +11 %, C3 +19 %, the shipped frame +50 %; gated at 0.1 scene units, C4 -3.6 %,
+// the others within noise (0.02 / 0.07 / 0.15 / 0.25 / 0.5 measured, profiles/r03_ab_shadow_wave_*).
+// Shadow rays are 59 % of C4's frame (profiles/r03_ab_noshadow_c4.log).  The stack is wave-uniform
+// and lives in the wave's BVH-stack LDS (no traversal of this wave is live during a shadow
+// query): one lane writes an entry, every lane reads it back as a broadcast.
+#ifndef TRT_SHADOW_WAVE
+#define TRT_SHADOW_WAVE 1
+#endif
+#ifndef TRT_SHADOW_WAVE_EXT
+#define TRT_SHADOW_WAVE_EXT 0.1
+#endif
+constexpr int kShadowWaveStack = 128; // >= kBvhStack
+__device__ __forceinline__ bool shadow_wave_q(const KArgs& A, f3 o, f3 d, f3 inv, float max_dist, float4* slab) {
+    typedef __attribute__((address_space(4))) const float cfloat;
+    typedef __attribute__((address_space(4))) const uint32_t cuint;
+    lds_u32* ws = (lds_u32*)reinterpret_cast<uint32_t*>(slab);
+    uint32_t sp = 0u, node = 0u;
+    for (;;) {
+        if (!(node & kBvhLeafBit)) {
+            const cfloat* R = (const cfloat*)(A.bvh4q + node);
+            const cuint* RC = (const cuint*)(A.bvh4q + node);
+            const uint32_t ex = RC[3];
+            const float sx = __uint_as_float((ex & 0xffu) << 23);
+            const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23);
+            const float sz = __uint_as_float(((ex >> 16) & 0xffu) << 23);
+            const float ax = (R[0] - o.x) * inv.x, bx = sx * inv.x;
+            const float ay = (R[1] - o.y) * inv.y, by = sy * inv.y;
+            const float az = (R[2] - o.z) * inv.z, bz = sz * inv.z;
+            const uint32_t qlx = RC[4], qly = RC[5], qlz = RC[6], qhx = RC[7], qhy = RC[8], qhz = RC[9];
+            const uint32_t nx = inv.x >= 0.0f ? qlx : qhx, fx = inv.x >= 0.0f ? qhx : qlx;
+            const uint32_t ny = inv.y >= 0.0f ? qly : qhy, fy = inv.y >= 0.0f ? qhy : qly;
+            const uint32_t nz = inv.z >= 0.0f ? qlz : qhz, fz = inv.z >= 0.0f ? qhz : qlz;
+            float key[4];
+            uint32_t r[4] = {RC[12], RC[13], RC[14], RC[15]};
+            uint32_t nh = 0u;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int sh = 8 * i;
+                const float tnx = __builtin_fmaf((float)((nx >> sh) & 0xffu), bx, ax);
+                const float tny = __builtin_fmaf((float)((ny >> sh) & 0xffu), by, ay);
+                const float tnz = __builtin_fmaf((float)((nz >> sh) & 0xffu), bz, az);
+                const float tfx = __builtin_fmaf((float)((fx >> sh) & 0xffu), bx, ax);
+                const float tfy = __builtin_fmaf((float)((fy >> sh) & 0xffu), by, ay);
+                const float tfz = __builtin_fmaf((float)((fz >> sh) & 0xffu), bz, az);
+                const float tn = fmaxf(fmaxf(tnx, tny), tnz);
+                const float tf = fminf(fminf(tfx, tfy), tfz);
+                const bool ok = tn <= tf && tf > TRT_EPS && tn <= max_dist;
+                const bool any = __ballot(ok) != 0ull;
+                // an entered child's key is finite (a NaN or infinite entry distance of that lane
+                // becomes 3e38), so entered children sort strictly before the missed ones (+inf)
+                const float k0 = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(tn)));
+                key[i] = any ? (k0 < 3.0e38f ? k0 : 3.0e38f) : __builtin_huge_valf();
+                nh += any ? 1u : 0u;
+            }
+            if (nh != 0u) {
+                // entered children nearest first (by the first walking lane's entry distance)
+#define TRT_CSWAP(a, b)                                   \
+    do {                                                  \
+        const bool sw = key[b] < key[a];                  \
+        const float ta = key[a], tb = key[b];             \
+        const uint32_t ra = r[a], rb = r[b];              \
+        key[a] = sw ? tb : ta;                            \
+        key[b] = sw ? ta : tb;                            \
+        r[a] = sw ? rb : ra;                              \
+        r[b] = sw ? ra : rb;                              \
+    } while (0)
+                TRT_CSWAP(0, 1);
+                TRT_CSWAP(2, 3);
+                TRT_CSWAP(0, 2);
+                TRT_CSWAP(1, 3);
+                TRT_CSWAP(1, 2);
+#undef TRT_CSWAP
+#pragma unroll
+                for (int k = 3; k >= 1; --k)
+                    if ((uint32_t)k < nh) {
+                        const uint32_t v = __builtin_amdgcn_readfirstlane(r[k]);
+                        if (lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) ws[sp] = v;
+                        ++sp;
+                    }
+                node = __builtin_amdgcn_readfirstlane(r[0]);
+                continue;
+            }
+        } else {
+            const uint32_t first = node & kBvhFirstMask;
+            const uint32_t n = ((node >> kBvhCountShift) & 15u) + 1u;
+            for (uint32_t k = first; k < first + n; ++k) {
+                const cfloat* T = (const cfloat*)(A.bvh_tris + k);
+                const f3 v0 = mk(T[0], T[1], T[2]), e1 = mk(T[3], T[4], T[5]), e2 = mk(T[6], T[7], T[8]);
+                // bvh_leaf's test, term for term
+                f3 hv = cross3(d, e2);
+                float a = dot3(e1, hv);
+                if (a > -TRT_EPS && a < TRT_EPS) continue;
+                float f = rcp_rn_lane(a);
+                f3 sv = sub(o, v0);
+                float u = f * dot3(sv, hv);
+                if (u < 0.0f || u > 1.0f) continue;
+                f3 q = cross3(sv, e1);
+                float v = f * dot3(d, q);
+                if (v < 0.0f || u + v > 1.0f) continue;
+                float t = f * dot3(e2, q);
+                if (t <= TRT_EPS) continue;
+                if (!(t < max_dist)) continue;
+                const uint32_t batch = __builtin_amdgcn_readfirstlane(__float_as_uint(T[10]));
+                const cfloat* B = (const cfloat*)(A.batches + batch);
+                const float bmin[3] = {B[0], B[1], B[2]}, bmax[3] = {B[3], B[4], B[5]};
+                if (aabb_hit(o, gate_inv(d), bmin, bmax)) return true;
+            }
+        }
+        if (sp == 0u) return false;
+        --sp;
+        node = __builtin_amdgcn_readfirstlane(ws[sp]);
+    }
 }
 
 template <bool COUNT, int GEOM>
@@ -966,6 +1159,20 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
     bool occluded = false;
     Hit unused;
     if (GEOM >= 2) {
+#if TRT_SHADOW_WAVE && TRT_BVH_QUANT
+        if constexpr (!COUNT && GEOM == 3 && TRT_BVH_WIDTH == 4 && slab_words<GEOM>() >= kShadowWaveStack)
+            if (A.bvh4q) {
+                // only when the walking lanes' origins lie within TRT_SHADOW_WAVE_EXT of the
+                // first one's (L-inf): scattered origins make the union of the walks far longer
+                // than any one of them
+                const float fx = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(o.x)));
+                const float fy = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(o.y)));
+                const float fz = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(o.z)));
+                const float e = fmaxf(fmaxf(fabsf(o.x - fx), fabsf(o.y - fy)), fabsf(o.z - fz));
+                if (__ballot(!(e <= (float)TRT_SHADOW_WAVE_EXT)) == 0ull)
+                    return shadow_wave_q(A, o, d, inv, max_dist, slab);
+            }
+#endif
         if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
         else trace_bvh<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     }
