@@ -142,8 +142,13 @@ def roofline(st_frame: dict, s_per_frame: float, envmap: bool, mesh: bool, pixel
         "flops_per_frame": flops, "us_per_frame": round(s_per_frame * 1e6, 3),
     }
     if kernel_ms_per_frame is not None:
-        out["kernel_us_per_frame"] = round(kernel_ms_per_frame * 1e3, 3)
-        out["kernel_frac"] = round(flops / (kernel_ms_per_frame * 1e-3) / 1e12 / VALU_PEAK_TFLOPS, 4)
+        if kernel_ms_per_frame * 1e-3 <= s_per_frame * 1.0001:
+            out["kernel_us_per_frame"] = round(kernel_ms_per_frame * 1e3, 3)
+            out["kernel_frac"] = round(flops / (kernel_ms_per_frame * 1e-3) / 1e12 / VALU_PEAK_TFLOPS, 4)
+        else:
+            # frames overlap (several in flight): a launch's span per frame is the frame's
+            # latency, longer than the wall time per frame, so it prices no rate
+            out["frame_span_us"] = round(kernel_ms_per_frame * 1e3, 3)
     ab = algorithmic_bytes(st_frame, pixels, envmap)
     out["hbm_index"] = {"algorithmic_bytes_per_frame": ab, "gb_s": round(ab / s_per_frame / 1e9, 2),
                         "peak": HBM_PEAK_GBS}

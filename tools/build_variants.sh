@@ -33,6 +33,7 @@ for v in "$@"; do
         g3lds12) variant g3lds12 -DTRT_G3_LDS=12 ;;
         ww1) variant ww1 -DTRT_WHILE_WHILE=1 ;;
         noswave) variant noswave -DTRT_SHADOW_WAVE=0 ;;
+        unode2) variant unode2 -DTRT_UNIFORM_NODE=2 ;;
         swe002) variant swe002 -DTRT_SHADOW_WAVE_EXT=0.02 ;;
         swe01) variant swe01 -DTRT_SHADOW_WAVE_EXT=0.1 ;;
         swe05) variant swe05 -DTRT_SHADOW_WAVE_EXT=0.5 ;;

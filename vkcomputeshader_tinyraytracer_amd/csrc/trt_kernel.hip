@@ -789,7 +789,24 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
             if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) return;
         }
         auto fetch = [&](uint32_t nd, float4& pe, uint4& qa, uint4& qb, uint4& ch) {
-#if TRT_UNIFORM_NODE
+#if TRT_UNIFORM_NODE == 2
+            // the first lane's node through scalar loads for every lane standing on it, the
+            // other lanes' nodes through per-lane loads (fewer lanes in the vector-memory pipe)
+            {
+                const uint32_t n0 = __builtin_amdgcn_readfirstlane(nd);
+                typedef __attribute__((address_space(4))) const float cfloat;
+                typedef __attribute__((address_space(4))) const uint32_t cuint;
+                const cfloat* R = (const cfloat*)(A.bvh4q + n0);
+                const cuint* RC = (const cuint*)(A.bvh4q + n0);
+                if (nd == n0) {
+                    pe = make_float4(R[0], R[1], R[2], R[3]);
+                    qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+                    qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+                    ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
+                    return;
+                }
+            }
+#elif TRT_UNIFORM_NODE
             // every lane at an internal node visits the same node (coherent rays, top levels):
             // one scalar fetch for the wave instead of 4 per-lane dwordx4 loads through TA/TD
             const uint32_t n0 = __builtin_amdgcn_readfirstlane(nd);
