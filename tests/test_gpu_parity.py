@@ -355,6 +355,53 @@ def test_multi_frame_launches_match_single_frames(gpu_renderer, config, sphere_e
     gpu_renderer.update_ubo(sc.ubo)
 
 
+@pytest.mark.parametrize("rot,skew,inter", [(1, 0, 0), (2, 3, 0), (0, 5, 0), (4, 1, 0), (0, 0, 1), (1, 3, 1)])
+@pytest.mark.parametrize("size", [(264, 200), (256, 128), (88, 56)])
+def test_xcd_dealing_knobs_match_single_frames(rot, skew, inter, size):
+    """TRT_XCD_ROT / TRT_XCD_SKEW / TRT_XCD_INTER re-deal a multi-frame launch's tiles to the
+    XCDs (rotated chunk classes per frame, diagonal classes, frames interleaved per chunk group):
+    a bijection, so every frame still equals
+    trt_render bit for bit — image sizes with leftover chunks, an odd tile column and row
+    (264x200), whole chunk rows (256x128) and fewer chunks than XCDs per row (88x56)."""
+    torch = pytest.importorskip("torch")
+    import os
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    old = {k: os.environ.get(k) for k in ("TRT_XCD_ROT", "TRT_XCD_SKEW", "TRT_XCD_INTER")}
+    os.environ["TRT_XCD_ROT"], os.environ["TRT_XCD_SKEW"], os.environ["TRT_XCD_INTER"] = str(rot), str(skew), str(inter)
+    try:
+        r = trt.Renderer(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        sc = S.CONFIGS["C2"](*size, env_size=SMALL_ENV)
+        p = sc.params()
+        r.upload_scene(sc)
+        n = 9
+        ubos = _moving_ubos(n)
+        fb = p.height * p.width * 4
+        out = torch.zeros((n, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        stream = torch.cuda.Stream()
+        r.set_stream(stream)
+        r.render_frames(p, out, n, ubos=ubos, frame_stride=fb, timing=True)
+        assert list(r.launch_frames()) == [n]
+        stream.synchronize()
+        r.set_stream(None)
+        got = out.cpu().numpy()
+        for i in range(n):
+            r.update_ubo(ubos[i])
+            one, _, _ = r.draw_frame(p)
+            assert np.array_equal(got[i], one), i
+    finally:
+        r.close()
+
+
 def test_frame_batch_bounds(gpu_renderer):
     for bad in (65, 1000):
         with pytest.raises(TrtError):

@@ -86,6 +86,7 @@ for v in "$@"; do
         wpb2) variant wpb2 -DTRT_WPB=2 ;;
         wpb4) variant wpb4 -DTRT_WPB=4 ;;
         bgearly) variant bgearly -DTRT_BG_EARLY ;;
+        noshare) variant noshare -DTRT_SHADOW_SHARE=0 ;;
         bgearly_wpb4) variant bgearly_wpb4 -DTRT_BG_EARLY -DTRT_WPB=4 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac

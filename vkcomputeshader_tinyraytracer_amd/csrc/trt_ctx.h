@@ -56,6 +56,10 @@ struct trt_ctx {
     std::vector<uint32_t> fev_nframes; // frames traced by each timed launch
     uint32_t frames_in_flight = TRT_FRAMES_IN_FLIGHT_DEFAULT;
     uint32_t frame_batch = TRT_FRAME_BATCH_AUTO; // frames per launch of a plain frame loop
+    // block -> tile dealing of multi-frame launches (trt_kernel.hip xcd_tile): rotation of the
+    // XCD chunk classes every 2^(xcd_rot - 1) frames (0 = fixed), per-chunk-row skew (0 = none);
+    // TRT_XCD_ROT / TRT_XCD_SKEW env
+    uint32_t xcd_rot = trt::kDefaultXcdRot, xcd_skew = trt::kDefaultXcdSkew, xcd_inter = trt::kDefaultXcdInter;
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;

@@ -197,6 +197,8 @@ struct SphereArg {
 // a launch share every UBO field but the camera position (the reference's interactive loop
 // moves only camPos, main.cpp:391-403, 2165-2179) and each writes its own image.
 constexpr uint32_t kMaxLaunchFrames = 64;
+// Tile dealing of multi-frame launches (trt_kernel.hip xcd_tile, trt_ctx xcd_rot / xcd_skew)
+constexpr uint32_t kDefaultXcdRot = 1, kDefaultXcdSkew = 0, kDefaultXcdInter = 0;
 struct FrameRec {
     float cam[3];      // UBO camPos (main.cpp:2170)
     uint32_t in_place; // band launch: rows written at their frame rows (TRT_FLAG_BAND_IN_PLACE)
@@ -240,6 +242,8 @@ struct KArgs {
     uint32_t ntx;                     // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
     uint32_t bvh_waves4;          // BVH walk: the 4-waves-per-SIMD build (GEOM 3)
+    uint32_t xcd_rot, xcd_skew;   // multi-frame tile dealing (xcd_tile): rotation period, row skew
+    uint32_t xcd_inter;           // ... frames interleaved per chunk group (inter_tile)
     // subtree split: this launch traces depths < split_d1; children at depth split_d1 become
     // tasks (split_d1 >= max_depth: no split).  split_w: the window (0 = split off).
     uint32_t split_w, split_d1;

@@ -552,7 +552,10 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
             c.bh += pass ? 1u : 0u;
         }
         if (!pass) continue;
-        if (SHADOW) return true;
+        if (SHADOW) {
+            h.idx = (int)k; // the occluder's BVH-ordered index (shared with the wave, trace_bvh4)
+            return true;
+        }
         best = t;
         h.t = t;
         h.kind = HIT_TRI;
@@ -563,6 +566,32 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
         h.ni = (int)__float_as_uint(cur.pad[2]);
     }
     return false;
+}
+
+// Shadow test of one triangle (BVH-ordered index k, wave-uniform) read through scalar loads:
+// bvh_leaf's test term for term (Moller-Trumbore, t in (MIN_EPSILON, max_dist), the reference's
+// batch gate), so a hit is a genuine occluder of this lane's query.
+__device__ __forceinline__ bool shadow_tri_s(const KArgs& A, uint32_t k, f3 o, f3 d, float max_dist) {
+    typedef __attribute__((address_space(4))) const float cfloat;
+    const cfloat* T = (const cfloat*)(A.bvh_tris + k);
+    const f3 v0 = mk(T[0], T[1], T[2]), e1 = mk(T[3], T[4], T[5]), e2 = mk(T[6], T[7], T[8]);
+    f3 hv = cross3(d, e2);
+    float a = dot3(e1, hv);
+    if (a > -TRT_EPS && a < TRT_EPS) return false;
+    float f = rcp_rn_lane(a);
+    f3 sv = sub(o, v0);
+    float u = f * dot3(sv, hv);
+    if (u < 0.0f || u > 1.0f) return false;
+    f3 q = cross3(sv, e1);
+    float v = f * dot3(d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    float t = f * dot3(e2, q);
+    if (t <= TRT_EPS) return false;
+    if (!(t < max_dist)) return false;
+    const uint32_t batch = __builtin_amdgcn_readfirstlane(__float_as_uint(T[10]));
+    const cfloat* B = (const cfloat*)(A.batches + batch);
+    const float bmin[3] = {B[0], B[1], B[2]}, bmax[3] = {B[3], B[4], B[5]};
+    return aabb_hit(o, gate_inv(d), bmin, bmax);
 }
 
 #ifndef TRT_BVH_WIDTH
@@ -706,6 +735,12 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 // 1 = while-while, 2 = speculative while-while (leaves parked until the wave has one each).
 #ifndef TRT_WHILE_WHILE
 #define TRT_WHILE_WHILE 0
+#endif
+// Shadow walks share found occluders across the wave (trace_bvh4's quantized walk, below).
+// Measured: C4 +0.7 %, C3 / shipped / README within noise (profiles/r03_ab_shadow_share.log;
+// the C4 shadow walks are long where they find nothing, not where they find late), so off.
+#ifndef TRT_SHADOW_SHARE
+#define TRT_SHADOW_SHARE 0
 #endif
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
@@ -883,6 +918,40 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
             if (node == kBvh4None) return;
         }
 #else
+#if TRT_SHADOW_SHARE
+        if constexpr (SHADOW && !COUNT) {
+            // Shared occluders: when lanes find an occluder in a step, every lane still walking
+            // tests the first one's triangle (scalar loads, no vector-memory instruction) and
+            // leaves if it is occluded by it too.  Neighbouring shading points asking about the
+            // same light are mostly shadowed by the same triangle, so one lane's find ends most
+            // of the wave's walks.  Any hit answers a shadow query (order-free) and the shared
+            // test is the leaf test itself, so the answer is the per-lane walk's.
+            for (;;) {
+                bool hit = false, more = false;
+                if (!(node & kBvhLeafBit)) {
+                    float4 pe;
+                    uint4 qa, qb, ch;
+                    fetch(node, pe, qa, qb, ch);
+                    more = visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c);
+                } else {
+                    hit = bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c);
+                }
+                const uint64_t m = __ballot(hit);
+                if (m != 0ull) {
+                    const uint32_t k = __builtin_amdgcn_readlane((uint32_t)h.idx, (int)__builtin_ctzll(m));
+                    if (!hit) hit = shadow_tri_s(A, k, o, d, max_dist);
+                    if (hit) {
+                        occluded = true;
+                        return;
+                    }
+                }
+                if (!more) {
+                    if (stack.sp == 0) return;
+                    node = stack.pop();
+                }
+            }
+        }
+#endif
         for (;;) {
             if (!(node & kBvhLeafBit)) {
                 float4 pe;
@@ -1069,28 +1138,8 @@ __device__ __forceinline__ bool shadow_wave_q(const KArgs& A, f3 o, f3 d, f3 inv
         } else {
             const uint32_t first = node & kBvhFirstMask;
             const uint32_t n = ((node >> kBvhCountShift) & 15u) + 1u;
-            for (uint32_t k = first; k < first + n; ++k) {
-                const cfloat* T = (const cfloat*)(A.bvh_tris + k);
-                const f3 v0 = mk(T[0], T[1], T[2]), e1 = mk(T[3], T[4], T[5]), e2 = mk(T[6], T[7], T[8]);
-                // bvh_leaf's test, term for term
-                f3 hv = cross3(d, e2);
-                float a = dot3(e1, hv);
-                if (a > -TRT_EPS && a < TRT_EPS) continue;
-                float f = rcp_rn_lane(a);
-                f3 sv = sub(o, v0);
-                float u = f * dot3(sv, hv);
-                if (u < 0.0f || u > 1.0f) continue;
-                f3 q = cross3(sv, e1);
-                float v = f * dot3(d, q);
-                if (v < 0.0f || u + v > 1.0f) continue;
-                float t = f * dot3(e2, q);
-                if (t <= TRT_EPS) continue;
-                if (!(t < max_dist)) continue;
-                const uint32_t batch = __builtin_amdgcn_readfirstlane(__float_as_uint(T[10]));
-                const cfloat* B = (const cfloat*)(A.batches + batch);
-                const float bmin[3] = {B[0], B[1], B[2]}, bmax[3] = {B[3], B[4], B[5]};
-                if (aabb_hit(o, gate_inv(d), bmin, bmax)) return true;
-            }
+            for (uint32_t k = first; k < first + n; ++k)
+                if (shadow_tri_s(A, k, o, d, max_dist)) return true; // bvh_leaf's test, term for term
         }
         if (sp == 0u) return false;
         --sp;
@@ -1918,16 +1967,27 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
 // 2x2-tile chunks (16x16 px) so neighbouring pixels' envmap texels and batch records hit
 // the same XCD L2.  Chunk c of XCD x is global chunk c*8+x; chunks are row-major over the
 // image in 2x2 tile units.  Bijective on [0, ntiles) (tail tiles map to themselves).
-__device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
+//
+// Frame f of a multi-frame launch can deal the chunk classes rotated (xcd_rot: class
+// (x + f / 2^(xcd_rot - 1)) mod 8 to XCD x) and skewed per chunk row (xcd_skew: row cy's chunk
+// columns shifted by xcd_skew * cy, diagonal classes).  Both are bijections of the chunks, so
+// every tile is traced once; they only move work between XCDs.  Why: the hardware deals blocks
+// to the XCDs round-robin, statically, so an XCD whose chunk class is costlier (the glass
+// spheres' stripes) finishes its share of a launch later than the others.
+__device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b, uint32_t f = 0) {
     const uint32_t tyn = A.ntiles / A.ntx;
     const uint32_t cw = A.ntx / 2u, ch = tyn / 2u;                 // whole 2x2 chunks
     const uint32_t nchunk = cw * ch, nfull = (nchunk / 8u) * 8u;   // dealt evenly to the XCDs
     auto chunk_tile = [&](uint32_t chunk, uint32_t sub) {
-        const uint32_t cx = chunk % cw, cy = chunk / cw;
+        uint32_t cx = chunk % cw;
+        const uint32_t cy = chunk / cw;
+        if (A.xcd_skew) cx = (cx + A.xcd_skew * cy) % cw;
         return (cy * 2u + sub / 2u) * A.ntx + cx * 2u + (sub % 2u);
     };
     if (b < nfull * 4u) {
-        const uint32_t j = b / 8u, x = b % 8u; // j-th block of XCD x
+        const uint32_t j = b / 8u; // j-th block of XCD x
+        uint32_t x = b % 8u;
+        if (A.xcd_rot) x = (x + (f >> (A.xcd_rot - 1u))) & 7u;
         return chunk_tile((j / 4u) * 8u + x, j % 4u);
     }
     // leftovers: the last nchunk % 8 chunks, then the odd right column, then the odd bottom row
@@ -1939,6 +1999,32 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b) {
     if (r < na) return r * A.ntx + (A.ntx - 1u);
     r -= na;
     return (ch * 2u) * A.ntx + r; // tile rows odd: the last tile row
+}
+
+// xcd_tile's fixed (unrotated) dealing
+__device__ __forceinline__ uint32_t xcd_tile_base(const KArgs& A, uint32_t b) { return xcd_tile(A, b, 0u); }
+
+// Frame-interleaved dealing of a multi-frame launch (xcd_inter): the launch walks the chunk
+// groups once, and each XCD traces chunk group g of every frame before group g + 1 (frame f's
+// chunk of group g rotated by f, so every XCD sees every chunk class).  All frames advance
+// together, so the launch ends on the last chunk groups of all frames instead of on the last
+// frame's whole tile order (whose costliest tiles then start near the end).  Sets f; tiles
+// outside whole chunk groups (leftovers) are dealt frame by frame after them.
+__device__ __forceinline__ uint32_t inter_tile(const KArgs& A, uint32_t vb, uint32_t& f) {
+    const uint32_t tyn = A.ntiles / A.ntx;
+    const uint32_t nchunk = (A.ntx / 2u) * (tyn / 2u), nfull = (nchunk / 8u) * 8u;
+    const uint32_t F = A.nframes, per = nfull * 4u; // blocks per frame in whole chunk groups
+    if (vb < F * per) {
+        const uint32_t x = vb % 8u, i = vb / 8u, q = i / 4u;
+        f = q % F;
+        const uint32_t g = q / F; // chunk group: chunks g * 8 .. g * 8 + 7
+        // block (g * 8 + ((x + f) & 7)) * 4 + i % 4 of frame f, in xcd_tile's unrotated dealing
+        const uint32_t c = (x + f) & 7u;
+        return xcd_tile_base(A, (g * 4u + i % 4u) * 8u + c);
+    }
+    const uint32_t r = vb - F * per, nl = A.ntiles - per;
+    f = r / nl;
+    return xcd_tile_base(A, per + r % nl);
 }
 
 // One 64-lane workgroup per 8x8 tile.  The hardware dispatcher hands each freed wave slot
@@ -2034,21 +2120,35 @@ __global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_ke
 #else
     // frame f = vb / ntiles of a multi-frame launch (plain frames only: split / deferred frames
     // and counting passes launch one frame)
-    uint32_t f = 0, t = vb;
+    uint32_t f = 0, t = vb, tile;
     if (!SPLIT && !DEFER && A.nframes > 1u) {
-        f = vb / A.ntiles;
-        t = vb - f * A.ntiles;
+        if (A.xcd_inter) {
+            tile = inter_tile(A, vb, f);
+        } else {
+            f = vb / A.ntiles;
+            t = vb - f * A.ntiles;
+            tile = xcd_tile(A, t, f);
+        }
+    } else {
+        tile = xcd_tile(A, t);
     }
-    trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], xcd_tile(A, t), cnt, lds, slab);
+    trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab);
 #endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
-    if (threadIdx.x == 0 && A.out32) {
+    // single-frame launches write the records to out32; multi-frame launches to the diagnostic
+    // buffer (trt_diag_set_buffer), with the frame in bits 20-27
+    float* clk = A.out32 ? A.out32 : reinterpret_cast<float*>(A.diag);
+    if (threadIdx.x == 0 && clk) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        uint32_t* rec = reinterpret_cast<uint32_t*>(A.out32) + 4 * (size_t)blockIdx.x;
+        uint32_t* rec = reinterpret_cast<uint32_t*>(clk) + 4 * (size_t)blockIdx.x;
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+#if !defined(TRT_PERSIST) && !defined(TRT_TPW)
+        rec[0] = (A.out32 ? xcd_tile(A, blockIdx.x) : (tile | (f << 20))) | ((xcc & 15u) << 28);
+#else
         rec[0] = xcd_tile(A, blockIdx.x) | ((xcc & 15u) << 28);
+#endif
         rec[1] = (uint32_t)t_start;
         rec[2] = (uint32_t)(t_end - t_start);
         rec[3] = (uint32_t)(t_start >> 32);

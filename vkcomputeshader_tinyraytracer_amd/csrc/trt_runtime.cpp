@@ -221,6 +221,9 @@ int trt_create(trt_ctx** out, int hip_device) {
         return TRT_ERR_HIP;
     }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
+    if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("TRT_XCD_SKEW")) c->xcd_skew = (uint32_t)std::min(7, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = std::atoi(e) != 0 ? 1u : 0u;
     *out = c;
     return TRT_OK;
 }
@@ -630,6 +633,9 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // everywhere: C4 2.90 vs 3.38 ms, C3 -9 %, shipped frame and README scene within 1 %
     // (profiles/r03_ab_waves4_after_stack_fix.log), so it is the default for every BVH scene.
     A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : 1u;
+    A.xcd_rot = c->xcd_rot;
+    A.xcd_skew = c->xcd_skew;
+    A.xcd_inter = c->xcd_inter;
     // 48-B nodes: for the 4-wave build (mode 1, the default), or for every BVH4 walk (mode 2)
     const int cm = bvh_compress_mode();
     A.bvh4c = (c->d_bvh4c && (cm == 2 || (cm == 1 && A.bvh_waves4))) ? c->d_bvh4c : nullptr;
