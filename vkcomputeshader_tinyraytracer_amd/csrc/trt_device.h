@@ -198,7 +198,7 @@ struct SphereArg {
 // moves only camPos, main.cpp:391-403, 2165-2179) and each writes its own image.
 constexpr uint32_t kMaxLaunchFrames = 64;
 // Tile dealing of multi-frame launches (trt_kernel.hip xcd_tile, trt_ctx xcd_rot / xcd_skew)
-constexpr uint32_t kDefaultXcdRot = 1, kDefaultXcdSkew = 0, kDefaultXcdInter = 0;
+constexpr uint32_t kDefaultXcdRot = 1, kDefaultXcdSkew = 0, kDefaultXcdInter = 1;
 struct FrameRec {
     float cam[3];      // UBO camPos (main.cpp:2170)
     uint32_t in_place; // band launch: rows written at their frame rows (TRT_FLAG_BAND_IN_PLACE)
