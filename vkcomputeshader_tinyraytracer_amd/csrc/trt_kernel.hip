@@ -1974,7 +1974,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
 // every tile is traced once; they only move work between XCDs.  Why: the hardware deals blocks
 // to the XCDs round-robin, statically, so an XCD whose chunk class is costlier (the glass
 // spheres' stripes) finishes its share of a launch later than the others.
-__device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b, uint32_t f = 0) {
+__device__ __forceinline__ uint32_t xcd_deal(const KArgs& A, uint32_t b, uint32_t roff) {
     const uint32_t tyn = A.ntiles / A.ntx;
     const uint32_t cw = A.ntx / 2u, ch = tyn / 2u;                 // whole 2x2 chunks
     const uint32_t nchunk = cw * ch, nfull = (nchunk / 8u) * 8u;   // dealt evenly to the XCDs
@@ -1987,7 +1987,7 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b, uint32_
     if (b < nfull * 4u) {
         const uint32_t j = b / 8u; // j-th block of XCD x
         uint32_t x = b % 8u;
-        if (A.xcd_rot) x = (x + (f >> (A.xcd_rot - 1u))) & 7u;
+        x = (x + roff) & 7u;
         return chunk_tile((j / 4u) * 8u + x, j % 4u);
     }
     // leftovers: the last nchunk % 8 chunks, then the odd right column, then the odd bottom row
@@ -2001,8 +2001,15 @@ __device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b, uint32_
     return (ch * 2u) * A.ntx + r; // tile rows odd: the last tile row
 }
 
-// xcd_tile's fixed (unrotated) dealing
-__device__ __forceinline__ uint32_t xcd_tile_base(const KArgs& A, uint32_t b) { return xcd_tile(A, b, 0u); }
+// Block b's tile with the chunk classes rotated for frame f of this launch (xcd_rot: by
+// f / 2^(xcd_rot - 1)).  Successive single-frame launches keep one dealing: rotating them too
+// (a per-launch offset) cost the shipped frame's 8 in-flight deferred frames +5 % (consecutive
+// frames' tiles on one XCD share its L2) for README -2 %, profiles/r03_ab_launch_off.log.
+__device__ __forceinline__ uint32_t xcd_tile(const KArgs& A, uint32_t b, uint32_t f = 0) {
+    return xcd_deal(A, b, A.xcd_rot ? (f >> (A.xcd_rot - 1u)) : 0u);
+}
+// the unrotated dealing
+__device__ __forceinline__ uint32_t xcd_tile_base(const KArgs& A, uint32_t b) { return xcd_deal(A, b, 0u); }
 
 // Frame-interleaved dealing of a multi-frame launch (xcd_inter): the launch walks the chunk
 // groups once, and each XCD traces chunk group g of every frame before group g + 1 (frame f's
