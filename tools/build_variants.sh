@@ -82,6 +82,7 @@ for v in "$@"; do
         noroot) variant noroot -DTRT_ROOT_SCALAR=0 ;;
         noempty) variant noempty -DTRT_BVH4_EMPTY_BOX=0 ;;
         g5) variant g5 -DTRT_G3_WAVES=5 -DTRT_G3_LDS=8 ;;
+        g3lds16) variant g3lds16 -DTRT_G3_LDS=16 -DTRT_G3_WAVES_SHALLOW=4 ;;
         g4s8) variant g4s8 -DTRT_G3_LDS=8 ;;
         wpb2) variant wpb2 -DTRT_WPB=2 ;;
         wpb4) variant wpb4 -DTRT_WPB=4 ;;

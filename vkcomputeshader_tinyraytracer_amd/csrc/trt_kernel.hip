@@ -345,13 +345,20 @@ __device__ __forceinline__ bool bvh_box(f3 o, f3 inv, const float* lo, const flo
 #endif
 constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 
-// GEOM 3 is the BVH walk compiled for 4 waves per SIMD (<= 128 VGPRs) with a 16-entry LDS
-// stack, so 16 waves fit a CU's LDS (16 x (4 KB stack + 6 KB deferred segments) = 160 KB).
+// GEOM 3 is the BVH walk compiled for 4 waves per SIMD (<= 128 VGPRs), or 5 (<= 96 VGPRs)
+// for plain frames of max_depth <= 4 (CAP <= 3, TRT_G3_WAVES_SHALLOW), with an 8-entry LDS
+// stack: 20 waves of (2 KB stack + 6 KB deferred segments) fill a CU's 160 KB.  8 and 16
+// entries tie at 4 waves (profiles/r03_ab_g3_lds_stack.log); 5 waves: C4 2.69 -> 2.63 ms,
+// depth-2 C4 -5.5 %, C3 within noise (profiles/r03_ab_g5.log).  CAP 4 (max_depth 5) needs
+// 8 KB of deferred segments and does not reach 5 waves, so deeper frames stay at 4.
 #ifndef TRT_G3_WAVES
 #define TRT_G3_WAVES 4
 #endif
+#ifndef TRT_G3_WAVES_SHALLOW
+#define TRT_G3_WAVES_SHALLOW 5
+#endif
 #ifndef TRT_G3_LDS
-#define TRT_G3_LDS 16
+#define TRT_G3_LDS 8
 #endif
 template <int GEOM>
 constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS : 0) : kBvhLdsStack; }
@@ -2066,11 +2073,13 @@ constexpr int slab_float4s() {
 #ifndef TRT_G0_WAVES
 #define TRT_G0_WAVES 5
 #endif
-template <int GEOM>
-constexpr int waves_per_simd() { return GEOM == 3 ? TRT_G3_WAVES : GEOM == 0 ? TRT_G0_WAVES : TRT_WAVES; }
+template <int GEOM, int CAP = 99>
+constexpr int waves_per_simd() {
+    return GEOM == 3 ? (CAP <= 3 ? TRT_G3_WAVES_SHALLOW : TRT_G3_WAVES) : GEOM == 0 ? TRT_G0_WAVES : TRT_WAVES;
+}
 
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
-__global__ __launch_bounds__(64 * TRT_WPB, waves_per_simd<GEOM>()) void trace_kernel(KArgs A) {
+__global__ __launch_bounds__(64 * TRT_WPB, (waves_per_simd<GEOM, ((SPLIT || DEFER) ? 99 : CAP)>())) void trace_kernel(KArgs A) {
 #if TRT_WPB > 1
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
     // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
