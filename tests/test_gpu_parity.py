@@ -355,12 +355,14 @@ def test_multi_frame_launches_match_single_frames(gpu_renderer, config, sphere_e
     gpu_renderer.update_ubo(sc.ubo)
 
 
-@pytest.mark.parametrize("rot,skew,inter", [(1, 0, 0), (2, 3, 0), (0, 5, 0), (4, 1, 0), (0, 0, 1), (1, 3, 1)])
+@pytest.mark.parametrize("rot,skew,inter,pair", [(1, 0, 0, 1), (2, 3, 0, 1), (0, 5, 0, 1), (4, 1, 0, 1), (0, 0, 1, 1),
+                                                (1, 3, 1, 1), (1, 0, 1, 2), (0, 3, 1, 2)])
 @pytest.mark.parametrize("size", [(264, 200), (256, 128), (88, 56)])
-def test_xcd_dealing_knobs_match_single_frames(rot, skew, inter, size):
+def test_xcd_dealing_knobs_match_single_frames(rot, skew, inter, pair, size):
     """TRT_XCD_ROT / TRT_XCD_SKEW / TRT_XCD_INTER re-deal a multi-frame launch's tiles to the
-    XCDs (rotated chunk classes per frame, diagonal classes, frames interleaved per chunk group):
-    a bijection, so every frame still equals
+    XCDs (rotated chunk classes per frame, diagonal classes, frames interleaved per chunk group)
+    and TRT_FRAME_GROUP=2 has a workgroup trace its tile in two consecutive frames (9 frames: the
+    last pair is one frame): a bijection, so every frame still equals
     trt_render bit for bit — image sizes with leftover chunks, an odd tile column and row
     (264x200), whole chunk rows (256x128) and fewer chunks than XCDs per row (88x56)."""
     torch = pytest.importorskip("torch")
@@ -368,8 +370,9 @@ def test_xcd_dealing_knobs_match_single_frames(rot, skew, inter, size):
 
     import vkcomputeshader_tinyraytracer_amd as trt
 
-    old = {k: os.environ.get(k) for k in ("TRT_XCD_ROT", "TRT_XCD_SKEW", "TRT_XCD_INTER")}
-    os.environ["TRT_XCD_ROT"], os.environ["TRT_XCD_SKEW"], os.environ["TRT_XCD_INTER"] = str(rot), str(skew), str(inter)
+    knobs = {"TRT_XCD_ROT": rot, "TRT_XCD_SKEW": skew, "TRT_XCD_INTER": inter, "TRT_FRAME_GROUP": pair}
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update({k: str(v) for k, v in knobs.items()})
     try:
         r = trt.Renderer(0)
     finally:

@@ -60,6 +60,7 @@ struct trt_ctx {
     // XCD chunk classes every 2^(xcd_rot - 1) frames (0 = fixed), per-chunk-row skew (0 = none);
     // TRT_XCD_ROT / TRT_XCD_SKEW env
     uint32_t xcd_rot = trt::kDefaultXcdRot, xcd_skew = trt::kDefaultXcdSkew, xcd_inter = trt::kDefaultXcdInter;
+    int frame_group = -1; // TRT_FRAME_GROUP (1 or 2); -1 = auto: 2 for triangle-free scenes, else 1
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;

@@ -2024,10 +2024,11 @@ __device__ __forceinline__ uint32_t xcd_tile_base(const KArgs& A, uint32_t b) { 
 // together, so the launch ends on the last chunk groups of all frames instead of on the last
 // frame's whole tile order (whose costliest tiles then start near the end).  Sets f; tiles
 // outside whole chunk groups (leftovers) are dealt frame by frame after them.
-__device__ __forceinline__ uint32_t inter_tile(const KArgs& A, uint32_t vb, uint32_t& f) {
+// F: the launch's frames (or frame pairs, frame_pair).
+__device__ __forceinline__ uint32_t inter_tile(const KArgs& A, uint32_t vb, uint32_t& f, uint32_t F) {
     const uint32_t tyn = A.ntiles / A.ntx;
     const uint32_t nchunk = (A.ntx / 2u) * (tyn / 2u), nfull = (nchunk / 8u) * 8u;
-    const uint32_t F = A.nframes, per = nfull * 4u; // blocks per frame in whole chunk groups
+    const uint32_t per = nfull * 4u; // blocks per frame in whole chunk groups
     if (vb < F * per) {
         const uint32_t x = vb % 8u, i = vb / 8u, q = i / 4u;
         f = q % F;
@@ -2138,8 +2139,21 @@ __global__ __launch_bounds__(64 * TRT_WPB, (waves_per_simd<GEOM, ((SPLIT || DEFE
     // and counting passes launch one frame)
     uint32_t f = 0, t = vb, tile;
     if (!SPLIT && !DEFER && A.nframes > 1u) {
-        if (A.xcd_inter) {
-            tile = inter_tile(A, vb, f);
+        if (A.xcd_inter && A.frame_group > 1u) {
+            // frame pairs: the block traces its tile in frames 2p and 2p + 1 (consecutive frames'
+            // tiles cost nearly the same, so the pairs keep the waves balanced) — half the
+            // workgroups, so half the per-workgroup launch and slot-refill overhead.  Two calls,
+            // not a loop over a group size: the loop form compiled to a slower kernel (C2 13.8 ->
+            // 14.9 us per frame, profiles/r03_ab_frame_group_loop.log)
+            uint32_t pr;
+            tile = inter_tile(A, vb, pr, (A.nframes + 1u) / 2u);
+            f = 2u * pr;
+            trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab);
+            if (f + 1u < A.nframes) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f + 1u], tile, cnt, lds, slab);
+            if (COUNT) flush_counts(A, cnt);
+            return;
+        } else if (A.xcd_inter) {
+            tile = inter_tile(A, vb, f, A.nframes);
         } else {
             f = vb / A.ntiles;
             t = vb - f * A.ntiles;
@@ -2510,7 +2524,9 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     }
     // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)
 #if !defined(TRT_PERSIST) && !defined(TRT_TPW) && TRT_WPB == 1
-    const dim3 fgrid(A.ntiles * std::max(A.nframes, 1u));
+    const uint32_t fblocks = A.nframes > 1u && A.xcd_inter && A.frame_group > 1u ? (A.nframes + 1u) / 2u
+                                                                                  : std::max(A.nframes, 1u);
+    const dim3 fgrid(A.ntiles * fblocks);
 #else
     const dim3 fgrid = grid;
 #endif

@@ -224,6 +224,7 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_SKEW")) c->xcd_skew = (uint32_t)std::min(7, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = std::atoi(e) != 0 ? 1u : 0u;
+    if (const char* e = std::getenv("TRT_FRAME_GROUP")) c->frame_group = std::min(2, std::max(1, std::atoi(e)));
     *out = c;
     return TRT_OK;
 }
@@ -636,6 +637,11 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.xcd_rot = c->xcd_rot;
     A.xcd_skew = c->xcd_skew;
     A.xcd_inter = c->xcd_inter;
+    // Frame groups (trace_kernel): triangle-free frames (C2) 14.8 -> 13.85 us per frame at
+    // 20-frame launches with pairs; mesh frames lose (C4 +2.5 %, C3 +10 %: their tiles' costs
+    // vary more from frame to frame and a pair doubles the longest wave),
+    // profiles/r03_ab_frame_pair.log
+    A.frame_group = c->frame_group > 0 ? (uint32_t)c->frame_group : (c->nbatch == 0 ? 2u : 1u);
     // 48-B nodes: for the 4-wave build (mode 1, the default), or for every BVH4 walk (mode 2)
     const int cm = bvh_compress_mode();
     A.bvh4c = (c->d_bvh4c && (cm == 2 || (cm == 1 && A.bvh_waves4))) ? c->d_bvh4c : nullptr;
