@@ -1,10 +1,10 @@
 """TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU oracle (oracle/liboracle.so).
 
 The oracle is a plain-C restatement of the reference hot path (shader.comp; see
-oracle/trt_oracle.c for the line-by-line citations and the parity status: "parity unpinned"
-against the running Vulkan reference, pinned by known-answer vectors, the literal-vs-fast
-mode equivalence, and reference-built input goldens).  Only tests/, __graft_entry__.smoke()
-and bench.py's cpu_baseline leg may import this module.
+oracle/trt_oracle.c for the line-by-line citations and the parity status: pinned to the
+reference's own Vulkan screenshots (tests/test_reference_screens.py), to known-answer
+vectors, by the literal-vs-fast mode equivalence, and by reference-built input goldens).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
 """
 from __future__ import annotations
 
