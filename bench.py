@@ -72,6 +72,10 @@ def parse():
                     help="frames of the tiled 3840x2160 leg (C4 row-tiled + RCCL gather on rank 0); 0 skips it")
     ap.add_argument("--extra-frames", type=int, default=40,
                     help="frames of the shipped / README-scene legs; 0 skips them")
+    ap.add_argument("--traffic", default="live", choices=["live", "table", "off"],
+                    help="roofline.traffic: live = two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over a "
+                         "child run of the same frame loop (N = 1); table = the committed measurement")
+    ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -438,6 +442,21 @@ def extra_frame(dev: int, name: str, frames: int, args) -> dict:
         "last_frame_matches_trt_render": res["last_frame_ok"],
         "roofline": roofline(mean, ms * 1e-3, True, True, p.width * p.height, res["kernel_ms_per_frame"]),
     }
+    if args.inflight == 0:
+        # the reference's frame pacing: MAX_FRAMES_IN_FLIGHT = 2 (main.cpp:45)
+        a2 = argparse.Namespace(**vars(args))
+        a2.inflight = 2
+        r2 = frame_loop(dev, sc, frames, 4, a2)
+        ms2 = r2["elapsed"] / frames * 1e3
+        out["at_2_in_flight"] = {
+            "note": "MAX_FRAMES_IN_FLIGHT = 2 (main.cpp:45), the reference's pacing; the leg above runs the "
+                    "library's auto count (8 for deferred-shadow frames)",
+            "ms_per_frame": round(ms2, 4), "fps": round(1e3 / ms2, 2),
+            "mray_s": round(r2["rays_total"] / r2["elapsed"] / 1e6, 3),
+            "latency_ms": round(r2["kernel_ms_per_frame"], 4),
+            "last_frame_matches_trt_render": r2["last_frame_ok"],
+        }
+        out["latency_ms"] = round(res["kernel_ms_per_frame"], 4)
     if name == "readme":
         out["published_context"] = {
             "fps": "10-11 (dips to 7)", "hardware": "NVIDIA GeForce RTX 4060", "source": "README.md:334-340",
@@ -511,9 +530,104 @@ def count_first(dev: int, scene) -> dict:
         _, _, st = r.draw_frame(scene.params(), count=True)
     return st
 
+# ---- physical HBM traffic (roofline.traffic) --------------------------------------------------
+
+TRAFFIC_TABLE = REPO / "profiles" / "r04_traffic_table.json"
+
+
+def traffic_probe(args) -> None:
+    """Child of measure_traffic, run under rocprofv3 --pmc: the N = 1 frame loop of the line
+    (same scene, camera walk, frames per launch) and nothing else."""
+    import torch
+
+    torch.cuda.set_device(0)
+    scene = make_scene(args.config)
+    res = frame_loop(0, scene, args.steps, args.warmup, args, check_last=False)
+    print(json.dumps({"probe_frames": args.steps, "launches": res["launches"]}), flush=True)
+
+
+def probe_steps(args) -> int:
+    """Frames of the probe: one timed-size launch (the auto frame batch caps a launch at 64)."""
+    return max(1, min(args.steps, 64))
+
+
+def _pmc_pass(counter: str, args, outdir: Path) -> list[dict]:
+    """One rocprofv3 PMC pass (one counter, --kernel-trace only) over the probe; returns the
+    per-dispatch records of the non-counting trace_kernel launches."""
+    import csv
+    import re
+    import subprocess
+
+    cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", str(outdir),
+           "-o", "run", "--", sys.executable, str(REPO / "bench.py"), "--traffic-probe", "--config", args.config,
+           "--steps", str(probe_steps(args)), "--warmup", str(args.warmup), "--inflight", str(args.inflight),
+           "--frame-batch", str(args.frame_batch), "--camera-period", str(args.camera_period)]
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    subprocess.run(cmd, check=True, timeout=240, env=env, cwd="/tmp", stdout=subprocess.DEVNULL,
+                   stderr=subprocess.DEVNULL)
+    rows: dict = {}
+    for f in outdir.rglob("run_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            if "trace_kernel" not in name or re.search(r"trace_kernel<\d+, true", name):
+                continue  # counting passes are not the timed kernel
+            d = rows.setdefault(r["Dispatch_Id"], {"grid": int(r["Grid_Size"]), "dur_ns":
+                                                  int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), "value": 0.0})
+            if r["Counter_Name"] == counter:
+                d["value"] += float(r["Counter_Value"])
+    return list(rows.values())
+
+
+def measure_traffic(args, kernel_us_per_frame: float | None) -> dict | None:
+    """HBM bytes per frame of the dominant kernel, from two separate PMC passes (FETCH_SIZE,
+    WRITE_SIZE; MI355X_MICROARCH.md §HBM: the two cannot share a pass) over a child run of the
+    line's own frame loop; the launches of the timed size (the largest grid) are kept.  FETCH_SIZE
+    and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE counts half the bytes of wide reads, so the
+    traffic is 2 x FETCH + WRITE (the raw figures are kept beside it)."""
+    import shutil
+    import tempfile
+
+    if args.traffic == "off":
+        return None
+    if args.traffic == "live" and shutil.which("rocprofv3"):
+        try:
+            with tempfile.TemporaryDirectory(prefix="trt_pmc_") as td:
+                fetch = _pmc_pass("FETCH_SIZE", args, Path(td) / "fetch")
+                write = _pmc_pass("WRITE_SIZE", args, Path(td) / "write")
+            gmax = max(d["grid"] for d in fetch)
+            f_sel = [d["value"] for d in fetch if d["grid"] == gmax]
+            w_sel = [d["value"] for d in write if d["grid"] == gmax]
+            frames = probe_steps(args) if args.frame_batch == 0 else min(probe_steps(args), args.frame_batch)
+            fetch_b = statistics.median(f_sel) * 1024 / frames
+            write_b = statistics.median(w_sel) * 1024 / frames
+            out = {"source": f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over a child run of "
+                             f"this frame loop, {len(f_sel)}+{len(w_sel)} launches of {frames} frames",
+                   "fetch_bytes_raw": round(fetch_b), "write_bytes": round(write_b)}
+        except Exception as e:  # the committed table stands in
+            out = {"live_error": f"{type(e).__name__}: {e}"}
+    else:
+        out = {}
+    if "fetch_bytes_raw" not in out:
+        if not TRAFFIC_TABLE.exists():
+            return out or None
+        t = json.loads(TRAFFIC_TABLE.read_text()).get(args.config)
+        if not t:
+            return out or None
+        out.update({"source": f"table: {TRAFFIC_TABLE.relative_to(REPO)} ({t.get('measured', '')})",
+                    "fetch_bytes_raw": t["fetch_bytes_raw"], "write_bytes": t["write_bytes"]})
+    out["bytes_per_frame"] = 2 * out["fetch_bytes_raw"] + out["write_bytes"]
+    if kernel_us_per_frame:
+        gbs = out["bytes_per_frame"] / (kernel_us_per_frame * 1e-6) / 1e9
+        out["hbm_gb_s"] = round(gbs, 1)
+        out["hbm_frac"] = round(gbs / HBM_PEAK_GBS, 4)
+    return out
+
 
 def main():
     args = parse()
+    if args.traffic_probe:
+        traffic_probe(args)
+        return
     import torch
 
     rank = int(os.environ.get("RANK", "0"))
@@ -601,8 +715,13 @@ def main():
                       "kernel_us_per_frame = HIP-event span of every launch / the frames it traced (one launch "
                       "traces many frames), from a second, untimed pass of the same loop.  Peak counts an FMA "
                       "as 2 flops; the kernel has no FMA contraction "
-                      "(-ffp-contract=off).  traffic: no PMC pass in this run (profiles/ holds this build's PMC "
-                      "summaries)")
+                      "(-ffp-contract=off).  traffic: HBM bytes per frame of trace_kernel from PMC "
+                      "(2 x FETCH_SIZE + WRITE_SIZE, see traffic_detail)")
+        if world == 1:
+            td = measure_traffic(args, rl.get("kernel_us_per_frame"))
+            if td and "bytes_per_frame" in td:
+                rl["traffic"] = td["bytes_per_frame"]
+            rl["traffic_detail"] = td
         result = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -6,7 +6,7 @@
 # tools/pmc_summary_r03.py.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/pmc_r03"
+OUT="${PMC_OUT:-$ROOT/gpurun_out/pmc_r03}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 P1="sq SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES"
