@@ -231,3 +231,59 @@ def test_render_multi_errors(multi):
         multi.render_frames(p, 2, outs=[small], frame_stride=48 * 64 * 4, ubos=_ubos(1))
     with pytest.raises(ValueError):
         multi.render_frames(p, 1, outs=[small, small])  # more outputs than local devices
+
+
+def test_failed_batch_allocation_then_retry(gpu_renderer, monkeypatch):
+    """A batch-buffer allocation that fails on slot 1 after slot 0 grew (TRT_TEST_FAIL_GROW=3:
+    slot-0 local, slot-0 gather, then slot-1 local fails) returns TRT_ERR_OOM; the agreement
+    frees both slots on every rank, so the retry of the same shape grows and agrees again and
+    renders correct frames instead of tracing into a half-grown slot."""
+    torch = pytest.importorskip("torch")
+    from vkcomputeshader_tinyraytracer_amd import TrtError
+
+    sc = S.config_c2(200, 120, env_size=ENV)
+    p = sc.params()
+    ubos = _ubos(4)
+    want = _single_frames(gpu_renderer, sc, p, ubos)
+    monkeypatch.setenv("TRT_TEST_FAIL_GROW", "3")
+    m = MultiRenderer([0])
+    monkeypatch.delenv("TRT_TEST_FAIL_GROW")
+    out = torch.zeros((4, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    try:
+        m.set_self_gather(True)
+        m.upload_scene(sc)
+        with pytest.raises(TrtError, match="injected"):
+            m.render_frames(p, 4, band_rows=8, root=0, frames_per_gather=2, outs=[out],
+                            frame_stride=p.height * p.width * 4, ubos=ubos)
+        m.synchronize()
+        m.render_frames(p, 4, band_rows=8, root=0, frames_per_gather=2, outs=[out],
+                        frame_stride=p.height * p.width * 4, ubos=ubos)
+        m.synchronize()
+    finally:
+        m.close()
+    got = out.cpu().numpy()
+    for i in range(4):
+        assert np.array_equal(got[i], want[i]), i
+
+
+def test_failed_host_frame_allocation_then_retry(gpu_renderer, monkeypatch):
+    """Host output: the frame buffer's growth (call 1) is agreed on by every rank before the
+    exchange; a failure is TRT_ERR_OOM on every rank (no rank is left in a send), and the retry
+    succeeds."""
+    from vkcomputeshader_tinyraytracer_amd import TrtError
+
+    sc = S.config_c3(160, 96, env_size=ENV)
+    want, _ = _whole(gpu_renderer, sc)
+    monkeypatch.setenv("TRT_TEST_FAIL_GROW", "1")
+    m = MultiRenderer([0])
+    monkeypatch.delenv("TRT_TEST_FAIL_GROW")
+    try:
+        m.upload_scene(sc)
+        out = np.zeros_like(want)
+        with pytest.raises(TrtError, match="injected"):
+            m.draw_frame(sc.params(), band_rows=8, outs=[out])
+        m.draw_frame(sc.params(), band_rows=8, outs=[out])
+    finally:
+        m.close()
+    assert np.array_equal(out, want)

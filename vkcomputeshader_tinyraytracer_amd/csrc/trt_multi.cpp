@@ -30,6 +30,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -74,6 +75,10 @@ struct trt_multi {
     bool have_scene = false;
     bool self_gather = false;
     bool broken = false; // a collective failed midway: the communicators are aborted
+    size_t frame_agreed = 0; // host-output frame bytes every rank's devices hold (agreed)
+    // Test hook (TRT_TEST_FAIL_GROW=k at creation): the k-th buffer growth of this context
+    // fails as if hipMalloc had, so tests can drive the failure paths on one GPU.
+    uint32_t grow_calls = 0, fail_grow_at = 0;
     int open_groups = 0; // RCCL groups opened by this context and not yet closed
     std::string err;
 };
@@ -198,6 +203,15 @@ void free_dev(trt_multi::Dev& d) {
 // buffer).  Returns false on failure (error text in m->err).
 bool grow(trt_multi* m, int device, uint8_t** p, size_t* cap, size_t bytes) {
     if (bytes <= *cap && *p) return true;
+    if (m->fail_grow_at && ++m->grow_calls == m->fail_grow_at) {
+        (void)hipSetDevice(device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        m->err = "multi-GPU buffer allocation: injected failure (TRT_TEST_FAIL_GROW)";
+        return false;
+    }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) {
@@ -212,6 +226,17 @@ bool grow(trt_multi* m, int device, uint8_t** p, size_t* cap, size_t bytes) {
     }
     *cap = bytes;
     return true;
+}
+
+// Frees both slots of a device's batch and gather buffers (capacities 0).
+void release_batch_buffers(trt_multi::Dev& d) {
+    if (hipSetDevice(d.device) == hipSuccess) (void)hipDeviceSynchronize();
+    for (int s = 0; s < 2; ++s) {
+        (void)hipFree(d.local[s]);
+        (void)hipFree(d.gather[s]);
+        d.local[s] = d.gather[s] = nullptr;
+        d.local_cap[s] = d.gather_cap[s] = 0;
+    }
 }
 
 // Sum over every device of every rank of `local` (one int per device of this process); the
@@ -295,9 +320,16 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
     // Buffers: every device sizes its batch buffer and a gather buffer for a root of every frame
     // (so the decision depends only on the batch shape, the same on every rank), both slots
     // together; when anything grows the ranks agree on the outcome before the first collective.
+    // The decision looks at both slots of both buffers, and a failed agreement frees them on
+    // every rank, so after a failure every rank grows (and agrees) again on the next call: the
+    // ranks' capacities never diverge (a half-grown slot would be traced into or skip the
+    // all-reduce its peers enter).
     const size_t need_local = L.local_bytes, need_gather = (size_t)nf * NG * blk;
     bool grows = false;
-    for (auto& d : m->devs) grows = grows || need_local > d.local_cap[0] || need_gather > d.gather_cap[0];
+    for (auto& d : m->devs)
+        for (int s = 0; s < 2; ++s)
+            grows = grows || need_local > d.local_cap[s] || need_gather > d.gather_cap[s] ||
+                    (need_local && !d.local[s]) || (need_gather && !d.gather[s]);
     if (grows) {
         std::vector<int> bad(m->devs.size(), 0);
         std::string why;
@@ -313,7 +345,10 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
         int total = 0;
         const int rc = agree(m, bad, total);
         if (rc != TRT_OK) return rc;
-        if (total) return mfail(m, TRT_ERR_OOM, why.empty() ? "a peer rank failed to allocate its batch buffers" : why);
+        if (total) {
+            for (auto& d : m->devs) release_batch_buffers(d);
+            return mfail(m, TRT_ERR_OOM, why.empty() ? "a peer rank failed to allocate its batch buffers" : why);
+        }
     }
     std::vector<uint32_t> froot(nf), fslot, fj;
     for (uint32_t f = 0; f < nf; ++f) froot[f] = trt_frame_root(rot0 + f, N, root);
@@ -342,7 +377,8 @@ int run_batch(trt_multi* m, const trt_params* p, const trt_ubo* ubos, uint32_t n
             const int rc = trt::render_frame_list(d.ctx, &q, fl.data(), nf, 0);
             if (rc != TRT_OK) {
                 d.ctx->stream = keep;
-                return mfail(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
+                // peers are about to enter the exchange with this rank: abort, don't strand them
+                return poison(m, rc, std::string("band render: ") + trt_last_error(d.ctx));
             }
         }
         d.ctx->stream = keep;
@@ -421,6 +457,7 @@ int trt_multi_create(trt_multi** out, const int* devices, uint32_t ndev) {
     if (!devices || ndev == 0) return TRT_ERR_INVALID;
     trt_multi* m = new (std::nothrow) trt_multi();
     if (!m) return TRT_ERR_OOM;
+    if (const char* e = std::getenv("TRT_TEST_FAIL_GROW")) m->fail_grow_at = (uint32_t)std::strtoul(e, nullptr, 10);
     m->nranks = ndev;
     m->devs.resize(ndev);
     std::vector<ncclComm_t> comms(ndev, nullptr);
@@ -456,6 +493,7 @@ int trt_multi_create_rank(trt_multi** out, int device, uint32_t nranks, uint32_t
     if (!id || nranks == 0 || rank >= nranks) return TRT_ERR_INVALID;
     trt_multi* m = new (std::nothrow) trt_multi();
     if (!m) return TRT_ERR_OOM;
+    if (const char* e = std::getenv("TRT_TEST_FAIL_GROW")) m->fail_grow_at = (uint32_t)std::strtoul(e, nullptr, 10);
     m->nranks = nranks;
     m->devs.resize(1);
     m->devs[0].device = device;
@@ -588,18 +626,36 @@ int trt_render_multi(trt_multi* m, const trt_params* p, uint32_t band_rows, int 
     const uint32_t r = trt_frame_root((uint32_t)(m->frame_seq++ % m->nranks), m->nranks, root);
     const bool dev_out = (p->flags & TRT_FLAG_DEVICE_PTRS) != 0;
     const size_t frame_bytes = (size_t)p->width * p->height * 4;
-    // host output: the root renders into its own device frame and copies it out
+    // host output: the root renders into its own device frame and copies it out.  Every rank
+    // may root a frame (rotation), so every device holds that frame buffer, and its growth is
+    // agreed on by all ranks before the exchange (the same decision on every rank: the frame
+    // size and the output mode, not who roots this frame).
+    if (!dev_out && frame_bytes > m->frame_agreed) {
+        std::vector<int> bad(m->devs.size(), 0);
+        std::string why;
+        for (size_t li = 0; li < m->devs.size(); ++li)
+            if (!grow(m, m->devs[li].device, &m->devs[li].frame, &m->devs[li].frame_cap, frame_bytes)) {
+                bad[li] = 1;
+                why = m->err;
+            }
+        int total = 0;
+        if ((rc = agree(m, bad, total)) != TRT_OK) return rc;
+        if (total) {
+            for (auto& d : m->devs) {
+                if (hipSetDevice(d.device) == hipSuccess) (void)hipDeviceSynchronize();
+                (void)hipFree(d.frame);
+                d.frame = nullptr;
+                d.frame_cap = 0;
+            }
+            m->frame_agreed = 0;
+            return mfail(m, TRT_ERR_OOM, why.empty() ? "a peer rank failed to allocate its frame buffer" : why);
+        }
+        m->frame_agreed = frame_bytes;
+    }
     std::vector<uint8_t*> outs(m->devs.size(), nullptr);
     for (size_t li = 0; li < m->devs.size(); ++li) {
         auto& d = m->devs[li];
-        if (d.rank == r && out8 && out8[li]) {
-            if (dev_out) {
-                outs[li] = out8[li];
-            } else {
-                if (!grow(m, d.device, &d.frame, &d.frame_cap, frame_bytes)) return TRT_ERR_OOM;
-                outs[li] = d.frame;
-            }
-        }
+        if (d.rank == r && out8 && out8[li]) outs[li] = dev_out ? out8[li] : d.frame;
     }
     if ((rc = fork_all(m)) != TRT_OK) return rc;
     if ((rc = run_batch(m, p, nullptr, 1, band_rows, (int)r, 0, outs.data(), 0)) != TRT_OK) return rc;

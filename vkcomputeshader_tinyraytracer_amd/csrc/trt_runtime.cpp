@@ -642,7 +642,7 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // vary more from frame to frame and a pair doubles the longest wave),
     // profiles/r03_ab_frame_pair.log
     A.frame_group = c->frame_group > 0 ? (uint32_t)c->frame_group : (c->nbatch == 0 ? 2u : 1u);
-    // 48-B nodes: for the 4-wave build (mode 1, the default), or for every BVH4 walk (mode 2)
+    // 48-B nodes (TRT_BVH_COMPRESS, opt-in; 0 = off is the default): for the 4-wave build (mode 1) or for every BVH4 walk (mode 2)
     const int cm = bvh_compress_mode();
     A.bvh4c = (c->d_bvh4c && (cm == 2 || (cm == 1 && A.bvh_waves4))) ? c->d_bvh4c : nullptr;
 }
