@@ -76,6 +76,9 @@ def parse():
                     help="roofline.traffic: live = two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over a "
                          "child run of the same frame loop (N = 1); table = the committed measurement")
     ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N > 1 process shape (torch.distributed nccl group + trt_multi rank "
+                         "communicator in one process, tiled headline) even at one rank (tests)")
     return ap.parse_args()
 
 
@@ -222,10 +225,10 @@ def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
 class Group:
     """torch.distributed helpers (no-ops at N = 1)."""
 
-    def __init__(self, world: int, rank: int):
+    def __init__(self, world: int, rank: int, force: bool = False):
         self.world, self.rank = world, rank
         self.dist = None
-        if world > 1:
+        if world > 1 or force:
             import torch
             import torch.distributed as dist
 
@@ -633,9 +636,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist_mode = world > 1 or args.force_dist  # the N > 1 process shape (also at one rank: tests)
     torch.cuda.set_device(local if world > 1 else 0)
     dev = torch.cuda.current_device()
-    g = Group(world, rank)
+    g = Group(world, rank, args.force_dist)
 
     from vkcomputeshader_tinyraytracer_amd import types as T
     from vkcomputeshader_tinyraytracer_amd.multi import ROOT_ROTATE, MultiRenderer
@@ -667,7 +671,7 @@ def main():
                                              if world == 1 else ""),
     }
     extra = {}
-    if world == 1:
+    if not dist_mode:
         value, ms_per_step, scaling = plain_value, fl["elapsed"] / K * 1e3, "weak"
         path = "trt_render_frames (plain frame loop, multi-frame launches)"
         parallelism = "1 GPU"
@@ -689,6 +693,17 @@ def main():
             "value": round(rays_s / el_s / 1e6, 3), "unit": "Mray/s", "ms_per_step": round(el_s / K * 1e3, 5),
             "frames": K, "frames_per_gather": fpg1, "last_frames_match_trt_render": ok_s,
             "workload": "one frame per step, row-tiled over all ranks (total work fixed as N grows)"}
+        # single-root forms: every frame assembled on rank 0, as the reference presents every frame
+        # from one queue (main.cpp:2207-2272); weak (N frames per step) and strong (one)
+        el_f, rays_f, _, ok_f = tiled_loop(g, dev, multi, scene, t_frames, args.warmup, args, fpg, 0)
+        el_fs, rays_fs, _, ok_fs = tiled_loop(g, dev, multi, scene, K, args.warmup, args, fpg1, 0)
+        extra["fixed_root"] = {
+            "weak": {"value": round(rays_f / el_f / 1e6, 3), "unit": "Mray/s", "ms_per_step": round(el_f / K * 1e3, 5),
+                     "frames": t_frames, "frames_per_gather": fpg, "last_frames_match_trt_render": ok_f},
+            "strong": {"value": round(rays_fs / el_fs / 1e6, 3), "unit": "Mray/s",
+                       "ms_per_step": round(el_fs / K * 1e3, 5), "frames": K, "frames_per_gather": fpg1,
+                       "last_frames_match_trt_render": ok_fs},
+            "workload": "every frame row-tiled over all ranks and gathered on rank 0 (the display GPU)"}
         st_frame, s_frame = mean_t, el_t / t_frames * world  # per-GPU wall time per frame of work
 
     tiled_c4 = tiled_frame(g, dev, multi, args.tiled_frames, args) if args.tiled_frames > 0 else None
@@ -698,7 +713,7 @@ def main():
     if args.extra_frames > 0:
         for key, name in (("shipped_frame", "ref"), ("readme_frame", "readme")):
             if rank == 0:
-                if world == 1:
+                if not dist_mode:
                     try:
                         extras[key] = extra_frame(dev, name, args.extra_frames, args)
                     except Exception as e:  # N = 1: report the failure in the line
@@ -708,7 +723,7 @@ def main():
             g.barrier()
 
     if rank == 0:
-        rl = roofline(st_frame, s_frame, envmap, mesh, pixels, fl["kernel_ms_per_frame"] if world == 1 else None)
+        rl = roofline(st_frame, s_frame, envmap, mesh, pixels, fl["kernel_ms_per_frame"] if not dist_mode else None)
         rl["kernel"] = "trace_kernel"
         rl["note"] = ("FP32 flops of one frame's executed work in SURVEY §8d units (counting passes of the camera "
                       "walk, mean per frame) / the wall time per frame of the timed loop (at N > 1: per GPU); "
@@ -717,7 +732,7 @@ def main():
                       "as 2 flops; the kernel has no FMA contraction "
                       "(-ffp-contract=off).  traffic: HBM bytes per frame of trace_kernel from PMC "
                       "(2 x FETCH_SIZE + WRITE_SIZE, see traffic_detail)")
-        if world == 1:
+        if not dist_mode:
             td = measure_traffic(args, rl.get("kernel_us_per_frame"))
             if td and "bytes_per_frame" in td:
                 rl["traffic"] = td["bytes_per_frame"]
@@ -749,7 +764,9 @@ def main():
                 "parallelism": parallelism,
                 "frames_per_step": world,
                 "launches": fl["launches"],
-                "last_frame_matches_trt_render": plain_ok if world == 1 else tiled_ok,
+                "last_frame_matches_trt_render": plain_ok if not dist_mode else tiled_ok,
+                "value_form": "frame per GPU, plain loop" if not dist_mode else
+                              "weak: N frames per step, each row-tiled over all ranks, rotating roots",
             },
             "roofline": rl,
         }
@@ -757,7 +774,7 @@ def main():
         if tiled_c4 is not None:
             result["tiled_frame"] = tiled_c4
         result.update(extras)
-        if world == 1 and not args.no_cpu:
+        if not dist_mode and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(scene, scene.params(), rays_of(count_first(dev, scene)),
                                                   args.cpu_seconds)
         print(json.dumps(result), flush=True)
