@@ -89,6 +89,9 @@ for v in "$@"; do
         bgearly) variant bgearly -DTRT_BG_EARLY ;;
         noshare) variant noshare -DTRT_SHADOW_SHARE=0 ;;
         bgearly_wpb4) variant bgearly_wpb4 -DTRT_BG_EARLY -DTRT_WPB=4 ;;
+        notrig) variant notrig -DTRT_DIAG_NO_UV_TRIG ;;
+        pool64) variant pool64 -DTRT_DEFER_POOL=64 ;;
+        pool192) variant pool192 -DTRT_DEFER_POOL=192 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac
 done

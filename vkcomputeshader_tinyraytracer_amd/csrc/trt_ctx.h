@@ -75,10 +75,9 @@ struct trt_ctx {
         trt::SplitCtr* ctr = nullptr;
         size_t npx = 0;  // pixels the buffers hold
         uint32_t cap = 0; // tasks per queue
-        // Deferred-shadow scratch (trt_set_deferred_shadows): event chunks + links, the
-        // shadow query queue, per-pixel log heads, the fallback list and the counters.
+        // Deferred-shadow scratch (trt_set_deferred_shadows): event chunks, the shadow query
+        // queue, per-pixel tree roots, the fallback list and the counters.
         float4* ev = nullptr;
-        uint32_t* ev_next = nullptr;
         float4* shq = nullptr;
         uint2* px_ev = nullptr;
         uint32_t* fb = nullptr;

@@ -159,18 +159,27 @@ struct SplitCtr {
 };
 
 // Deferred-shadow frame (trt_set_deferred_shadows).  Pass A traces every pixel's Whitted tree
-// without its shadow rays and logs, per DFS step, one colour event (in the reference's pop
-// order) into a chunked per-lane log; the shadow queries go to one dense queue that pass B
-// traces with every lane busy; pass C replays each pixel's events in order.  A chunk holds
-// kEvRows events of the 64 lanes of a wave, laid out [row][plane][lane] (4 x 16 B planes per
-// event, coalesced across lanes); ev_next[chunk * 64 + lane] links a lane's chunks.
+// without its shadow rays and logs one colour event per traced segment; the shadow queries go
+// to one dense queue that pass B traces with every lane busy; pass C sums each pixel's events
+// in the reference's pop order.  The events of a pixel form its segment TREE: an event names
+// the children its segment made (tag bits) and each child, wherever and whenever it is traced,
+// writes its own event's slot into its parent's plane 3 (z = reflection child, w = refraction
+// child).  So pass A may trace a pixel's segments in any order and on any lane of the wave (the
+// lanes share their pending segments, defer_walk), and pass C walks the tree in the pop order
+// of shader.comp:530-575 (node, reflection subtree, refraction subtree).  A chunk holds kEvRows
+// events of the 64 lanes of a wave, laid out [row][plane][lane] (4 x 16 B planes per event,
+// coalesced across lanes); a slot is (chunk * kEvRows + row) * 64 + lane.
+//   plane 0: kd.xyz, tag            (tag & kEvTagConst: xyz = the event's colour term)
+//   plane 1: diffuse terms[3], albedo.x
+//   plane 2: specular terms[3], albedo.y
+//   plane 3: throughput, occluded-light bits (pass B), reflection child, refraction child
 constexpr uint32_t kEvRows = 4u;
-constexpr uint32_t kEvNone = 0xFFFFFFFFu;  // px_ev.x of a pixel re-traced by defer_fallback
-constexpr uint32_t kEvConst = 0xFFFFFFFFu; // plane0.w of an event whose colour is known in pass A
-// plane0.w of a LINK event (deferred frames with a subtree split): "here come the events of a
-// subtree traced by another lane", plane0 = (first chunk, events, lane, kEvLink) of its chain.
-constexpr uint32_t kEvLink = 0xFFFFFFFEu;
-constexpr uint32_t kMaxLinkDepth = 20u; // nested subtree chains: max_depth / window <= 20
+constexpr uint32_t kEvNone = 0xFFFFFFFFu;      // px_ev.x of a pixel re-traced by defer_fallback
+constexpr uint32_t kEvTagConst = 0x80000000u;  // tag bit: colour term known in pass A
+constexpr uint32_t kEvTagRefl = 1u << 3;       // tag bit: the segment made a reflection child
+constexpr uint32_t kEvTagRefr = 1u << 4;       // tag bit: ... a refraction (or TIR) child
+constexpr uint32_t kEvRoot = 0xFFFFFFFFu;      // parent link of a root segment
+constexpr uint32_t kMaxTreeDepth = 20u;        // MAX_DEPTH: pass C's stack of refraction children
 // The event pool and the query queue are split into kDeferStripes stripes (tile t allocates
 // from stripe hash(t), each with its own counter on its own 64-B line): one counter
 // for a whole 4K frame serialises ~10^6 wave-aggregated atomics in one L2 channel (measured:
@@ -253,7 +262,7 @@ struct KArgs {
     Task* __restrict__ q_out;         // tasks this launch produces
     const Task* __restrict__ q_in;    // tasks this launch consumes (trace_tasks)
     Task* __restrict__ q_buf[2];      // the two queues of the slot (ping-pong)
-    uint32_t* __restrict__ q_link_out; // deferred split: per task of q_out, its LINK event slot
+    uint32_t* __restrict__ q_link_out; // deferred split: per task of q_out, its parent link (slot << 1 | refr)
     const uint32_t* __restrict__ q_link_in;
     uint32_t* __restrict__ q_link_buf[2];
     uint32_t* __restrict__ q_out_n;   // produced count of q_out
@@ -269,9 +278,8 @@ struct KArgs {
     uint32_t ev_cap;                  // event chunks per stripe (stripe s: chunks [s * ev_cap, ...))
     uint32_t shq_cap;                 // queries per stripe (stripe s: queries [s * shq_cap, ...))
     float4* __restrict__ ev;          // chunks of kEvRows x 4 planes x 64 lanes float4
-    uint32_t* __restrict__ ev_next;   // per chunk and lane: the lane's next chunk
     float4* __restrict__ shq;         // per query: (origin, max distance), (direction, slot << 2 | light)
-    uint2* __restrict__ px_ev;        // per output pixel: (first chunk or kEvNone, events)
+    uint2* __restrict__ px_ev;        // per output pixel: (root event slot or kEvNone, 0)
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
     FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch

@@ -1285,8 +1285,13 @@ __device__ __forceinline__ EnvFetch env_fetch(const KArgs& A, f3 d) {
         return EnvFetch{0u, 0xffu, 0xff00u, 0xff0000u, u, v};
     }
 #endif
+#ifdef TRT_DIAG_NO_UV_TRIG
+    // diagnostic: prices atan2 / acos (wrong texels, same memory pattern class)
+    float theta = d.z * 3.0f, phi = (d.y + 1.0f) * 1.5f;
+#else
     float theta = atan2f(d.z, d.x);
     float phi = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
+#endif
     // direction_to_uv, shader.comp:410-416.  atan/acos are already ocml's (within a few ulp
     // of the oracle's libm, tests/helpers.py FLOAT_TOL), so the two divisions by constants
     // are products with the rounded reciprocals (<= 1 ulp apart from the quotients).
@@ -1471,7 +1476,7 @@ struct StackOf<CAP, true> {
 
 // Wave-aggregated append of up to two tasks per lane (one atomic per wave).  A task that does
 // not fit the queue is not written and its flag is cleared: the caller traces it in place.
-// DEFER: each task also carries the LINK event slot (la / lb) its chain head goes to.
+// DEFER: each task also carries its parent link (la / lb: parent event slot << 1 | refraction).
 template <bool DEFER = false>
 __device__ __forceinline__ void enqueue2(const KArgs& A, bool& sa, const Seg& a, bool& sb, const Seg& b,
                                          uint32_t pixel, uint32_t la = 0, uint32_t lb = 0) {
@@ -1509,17 +1514,18 @@ __device__ __forceinline__ float from_fixed(unsigned long long v) {
     return (float)((double)(long long)v * (1.0 / 4294967296.0));
 }
 
-// ---- deferred shadows: the per-lane event log (trt_device.h kEvRows) ---------------------
+// ---- deferred shadows: the per-lane event pool (trt_device.h kEvRows) --------------------
 struct EvLog {
-    uint32_t stripe = 0;     // the stripe of the event pool and query queue (wave-uniform)
-    uint32_t k = 0;          // events this lane has logged
-    uint32_t chunk = 0;      // the chunk holding event k - 1
-    uint32_t first = kEvNone;
-    bool ovf = false;        // event pool or query queue full: defer_fallback re-traces the pixel
+    uint32_t stripe = 0; // the stripe of the event pool and query queue (wave-uniform)
+    uint32_t k = 0;      // events this lane has logged
+    uint32_t chunk = 0;  // the chunk holding event k - 1
+    bool ovf = false;    // event pool or query queue full: the lane's pixels go to defer_fallback
 };
 
-// Slot of this lane's next event; every active lane calls it once per DFS step.  Lanes that
-// start a chunk together share one (wave-aggregated atomic); each lane links its own chain.
+// Slot of this lane's next event; pass A calls it on every lane once per step of the wave.
+// Lanes that start a chunk together share one (each lane owns its column of a chunk; one
+// wave-aggregated atomic).  A slot only names where the event lives: the tree links (plane 3)
+// give the order, so chunks are not chained.
 __device__ __forceinline__ uint32_t ev_alloc(const KArgs& A, EvLog& L) {
     const uint32_t row = L.k % kEvRows;
     const bool need = row == 0u && !L.ovf;
@@ -1530,14 +1536,8 @@ __device__ __forceinline__ uint32_t ev_alloc(const KArgs& A, EvLog& L) {
         if ((int)lane_id() == leader) base = atomicAdd(&A.dctr->chunks[L.stripe * kCtrStride], 1u);
         base = __shfl(base, leader, 64);
         if (need) {
-            if (base >= A.ev_cap) {
-                L.ovf = true;
-            } else {
-                base += L.stripe * A.ev_cap;
-                if (L.k == 0u) L.first = base;
-                else A.ev_next[(size_t)L.chunk * 64u + lane_id()] = base;
-                L.chunk = base;
-            }
+            if (base >= A.ev_cap) L.ovf = true;
+            else L.chunk = base + L.stripe * A.ev_cap;
         }
     }
     ++L.k;
@@ -1548,30 +1548,134 @@ __device__ __forceinline__ float4* ev_plane(const KArgs& A, uint32_t s, uint32_t
     return A.ev + ((size_t)(s >> 6) * 4u + p) * 64u + (s & 63u);
 }
 
+// The closest hit's shading inputs (shader.comp:302-360): point, normal, material.
+struct Surf {
+    f3 p, n;
+    float alb[4], kd[3], sexp, ior;
+};
+
+template <bool COUNT>
+__device__ __forceinline__ Surf resolve_hit(const KArgs& A, const Seg& cur, const Hit& h, Cnt& cnt) {
+    Surf s;
+    s.p = add(cur.o, muls(cur.d, h.t));
+    if (h.kind == HIT_FLOOR) {
+        s.n = mk(0.0f, 1.0f, 0.0f);
+        float c0 = 0.3f, c1 = 0.3f, c2 = 0.3f;
+        if (A.flags & TRT_FLAG_CHECKER) { // shader.comp:312
+            float m = floorf(s.p.x * 0.5f + 1024.0f) + floorf(s.p.z * 0.5f);
+            float mod2 = m - 2.0f * floorf(m / 2.0f);
+            if (!(mod2 == 0.0f)) {
+                c1 = 0.2f;
+                c2 = 0.1f;
+            }
+        }
+        s.alb[0] = 2.0f; s.alb[1] = 0.0f; s.alb[2] = 0.0f; s.alb[3] = 0.0f;
+        s.kd[0] = c0; s.kd[1] = c1; s.kd[2] = c2;
+        s.sexp = 1.0f;
+        s.ior = 1.0f;
+    } else if (h.kind == HIT_SPHERE) {
+        const SphereArg& sp = A.sph[h.idx];
+        s.n = normalize3(sub(s.p, mk(sp.c[0], sp.c[1], sp.c[2])));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s.alb[k] = sp.m.albedo[k];
+        s.kd[0] = sp.m.kd[0]; s.kd[1] = sp.m.kd[1]; s.kd[2] = sp.m.kd[2];
+        s.sexp = sp.m.spec_exp;
+        s.ior = sp.m.ior;
+    } else {
+        if (COUNT) ++cnt.trin;
+        const TriShade& ts = A.shade[h.idx];
+        if (h.ni == 0) {
+            const TriGeo& g = A.geo[h.idx];
+            s.n = normalize3(cross3(ld3(g.e1), ld3(g.e2)));
+        } else {
+            float w = 1.0f - h.u - h.v;
+            f3 nn = add(add(muls(ld3(ts.n0), w), muls(ld3(ts.n1), h.u)), muls(ld3(ts.n2), h.v));
+            s.n = normalize3(nn);
+        }
+        const Mat& m = A.mats[ts.material];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s.alb[k] = m.albedo[k];
+        s.kd[0] = m.kd[0]; s.kd[1] = m.kd[1]; s.kd[2] = m.kd[2];
+        s.sexp = m.spec_exp;
+        s.ior = m.ior;
+    }
+    return s;
+}
+
+// One light of the Phong loop (shader.comp:491-505): direction, distance, shadow origin and the
+// diffuse / specular terms; `matters`: a light whose two terms both vanish from the colour (a
+// zero term, or a zero albedo weight: diffuse * 0 = 0 for any finite diffuse) adds exactly
+// nothing lit or shadowed, so its shadow query cannot change the pixel and a frame does not
+// trace it.  The counting pass keeps the reference's behaviour (traces it and adds the terms
+// when lit: its counters and image are the reference's, and tests/test_gpu_parity.py checks
+// that its image equals the frame's bit for bit) and reports the skipped queries and their work.
+struct LightTerm {
+    f3 ld, so;
+    float dist, diff, spec;
+    bool matters;
+};
+
+__device__ __forceinline__ LightTerm light_term(const KArgs& A, const Surf& s, f3 v, int i) {
+    LightTerm t;
+    f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
+    t.ld = normalize3(sub(L, s.p));
+    t.dist = length3(sub(L, s.p));
+    t.so = dot3(t.ld, s.n) < 0.0f ? sub(s.p, muls(s.n, TRT_EPS)) : add(s.p, muls(s.n, TRT_EPS));
+    t.diff = 1.0f * fmaxf(0.0f, dot3(s.n, t.ld));
+    const f3 rdir = reflect3(neg(t.ld), s.n);
+#ifdef TRT_DIAG_NO_POW
+    t.spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * s.sexp; // diagnostic: prices powf
+#else
+    t.spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), s.sexp);
+#endif
+    t.matters = TRT_SKIP_DARK == 0 || (s.alb[0] != 0.0f && t.diff != 0.0f) || (s.alb[1] != 0.0f && t.spec != 0.0f);
+    return t;
+}
+
+// Children (shader.comp:509-575).  Children that the reference would push and then drop unseen
+// at the depth / throughput test (shader.comp:449) are not made (mk_* false).
+__device__ __forceinline__ void make_children(const Seg& cur, const Surf& s, int D, Seg& refr, bool& mk_refr,
+                                              Seg& refl, bool& mk_refl) {
+    const int cd = cur.depth + 1;
+    mk_refr = mk_refl = false;
+    bool skip_reflect = false;
+    if (s.alb[3] > 0.0f) {
+        f3 rd = custom_refract(cur.d, s.n, s.ior, 1.0f);
+        if (length3(rd) > 0.0001f) {
+            rd = normalize3(rd);
+        } else { // total internal reflection: one reflected child, shader.comp:533-555
+            rd = normalize3(reflect3(cur.d, s.n));
+            skip_reflect = true;
+        }
+        f3 off = dot3(rd, s.n) < 0.0f ? muls(neg(s.n), TRT_EPS) : muls(s.n, TRT_EPS);
+        refr = Seg{add(s.p, off), rd, cur.thr * s.alb[3], cd};
+        float tt = (refr.thr * refr.thr + refr.thr * refr.thr) + refr.thr * refr.thr;
+        mk_refr = cd < D && !(tt < 0.001f);
+    }
+    if (s.alb[2] > 0.0f && !skip_reflect) {
+        f3 rd = normalize3(reflect3(cur.d, s.n));
+        f3 off = dot3(rd, s.n) < 0.0f ? muls(neg(s.n), TRT_EPS) : muls(s.n, TRT_EPS);
+        refl = Seg{add(s.p, off), rd, cur.thr * s.alb[2], cd};
+        float tt = (refl.thr * refl.thr + refl.thr * refl.thr) + refl.thr * refl.thr;
+        mk_refl = cd < D && !(tt < 0.001f);
+    }
+}
+
 // The DFS of one segment tree (root = a primary ray, or a task of a split launch).  Returns
 // the unclamped colour sum in the reference's pop order.  SPLIT: children at depth
 // >= A.split_d1 are handed to the task queue (`spilled` is set) instead of being traced.
-// DEFER: no shadow ray is traced and nothing is summed; each step logs its colour event into
-// *elog (a miss's or an unlit hit's colour term, or a hit's Phong terms with the lights whose
-// shadow queries it appended to A.shq) for defer_resolve to sum in this same order.  HYB:
-// the deferred refraction children live in CAP LDS entries plus a private tail.
-template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
+// HYB: the deferred refraction children live in CAP LDS entries plus a private tail.  (The
+// shading here is written out rather than through resolve_hit / light_term / make_children:
+// the factored form compiles the C2 and C4 kernels with more live registers — C2 spilled.)
+template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool HYB = SPLIT>
 __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float* lds, float4* slab,
-                                       uint32_t pixel, bool& spilled, EvLog* elog = nullptr) {
-#ifdef TRT_BG_EARLY
-    static_assert(!DEFER, "TRT_BG_EARLY (diagnostic) does not log deferred events");
-#endif
+                                       uint32_t pixel, bool& spilled) {
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
     using Stk = typename StackOf<CAP, HYB>::type;
     typename Stk::Mem stk_mem;
     Stk stk(lds, stk_mem);
     for (;;) {
-        uint32_t slot = 0;
-        if (DEFER) {
-            slot = ev_alloc(A, *elog);
-            if (elog->ovf) break;
-        }
         if (COUNT && cur.depth > 0) ++cnt.sec;
 #ifdef TRT_DIAG_PIXEL_WORK
         ++cnt.wseg;
@@ -1597,12 +1701,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             if (!env_miss) color = add(color, muls(mk(0.2f, 0.7f, 0.8f), cur.thr));
 #else
             f3 bg = background(A, cur.d);
-            if (DEFER) {
-                const f3 c = muls(bg, cur.thr);
-                *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvConst));
-            } else {
-                color = add(color, muls(bg, cur.thr));
-            }
+            color = add(color, muls(bg, cur.thr));
 #endif
         } else {
             // Resolve the closest hit: point, normal, material (shader.comp:302-360).
@@ -1654,8 +1753,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             f3 v = neg(cur.d);
             f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
             f3 kdv = mk(kd[0], kd[1], kd[2]);
-            float dterm[3] = {0.0f, 0.0f, 0.0f}, sterm[3] = {0.0f, 0.0f, 0.0f};
-            uint32_t qmask = 0; // DEFER: lights whose shadow query went to A.shq
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
@@ -1680,28 +1777,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                                      (alb[1] != 0.0f && spec != 0.0f);
                 if (COUNT) ++cnt.sh;
                 if (!COUNT && !matters) continue;
-                if (DEFER) {
-                    // Append the query (lanes of one light together: neighbouring queries of
-                    // the dense pass-B queue share a light and nearby origins).
-                    const uint64_t m = __ballot(true);
-                    const int leader = __ffsll((unsigned long long)m) - 1;
-                    uint32_t base = 0;
-                    if ((int)lane_id() == leader)
-                        base = atomicAdd(&A.dctr->nq[elog->stripe * kCtrStride], (uint32_t)__popcll(m));
-                    base = __shfl(base, leader, 64);
-                    const uint32_t qi = base + lane_rank(m);
-                    if (qi < A.shq_cap) {
-                        float4* q = A.shq + 2 * ((size_t)elog->stripe * A.shq_cap + qi);
-                        q[0] = make_float4(so.x, so.y, so.z, dist);
-                        q[1] = make_float4(ld.x, ld.y, ld.z, __uint_as_float((slot << 2) | (uint32_t)i));
-                        qmask |= 1u << i;
-                        dterm[i] = diff;
-                        sterm[i] = spec;
-                    } else {
-                        elog->ovf = true;
-                    }
-                    continue;
-                }
                 const Cnt before = cnt;
                 const bool occl = shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab);
                 if (COUNT && !matters) {
@@ -1717,20 +1792,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 diffuse = add(diffuse, muls(kdv, diff));
                 specular = add(specular, muls(kdv, spec));
             }
-            if (DEFER) {
-                if (elog->ovf) break;
-                if (qmask == 0u) { // no light can add anything: the colour term is known now
-                    const f3 c = muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr);
-                    *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvConst));
-                } else { // pass B ORs the occluded lights into plane 3's second word
-                    *ev_plane(A, slot, 0) = make_float4(kd[0], kd[1], kd[2], __uint_as_float(qmask));
-                    *ev_plane(A, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], alb[0]);
-                    *ev_plane(A, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], alb[1]);
-                    *reinterpret_cast<float2*>(ev_plane(A, slot, 3)) = make_float2(cur.thr, 0.0f);
-                }
-            } else {
-                color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
-            }
+            color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
             // Children (shader.comp:509-575).  Children that the reference would push and
             // then drop unseen at the depth / throughput test (shader.comp:449) are not made.
             const int cd = cur.depth + 1;
@@ -1757,22 +1819,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 float tt = (refl.thr * refl.thr + refl.thr * refl.thr) + refl.thr * refl.thr;
                 mk_refl = cd < D && !(tt < 0.001f);
             }
-            if (SPLIT && DEFER && cd >= (int)A.split_d1) {
-                // window edge of a deferred frame: both children become tasks, and this lane's
-                // log gets a LINK event per task at the place of the child's events (reflection
-                // subtree first, as the reference pops it first)
-                bool sa = mk_refl, sb = mk_refr;
-                uint32_t la = 0, lb = 0;
-                if (sa) la = ev_alloc(A, *elog);
-                if (sb) lb = ev_alloc(A, *elog);
-                if (elog->ovf) break;
-                enqueue2<true>(A, sa, refl, sb, refr, pixel, la, lb);
-                if (sa != mk_refl || sb != mk_refr) { // task queue full: re-trace the pixel
-                    elog->ovf = true;
-                    break;
-                }
-                mk_refl = mk_refr = false;
-            } else if (SPLIT && cd >= (int)A.split_d1) { // window edge: both children become tasks
+            if (SPLIT && cd >= (int)A.split_d1) { // window edge: both children become tasks
                 bool sa = mk_refl, sb = mk_refr;
                 enqueue2(A, sa, refl, sb, refr, pixel);
                 if (sa) mk_refl = false;
@@ -1801,6 +1848,205 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
         }
     }
     return color;
+}
+
+// ---- deferred shadows, pass A: the wave's shared segment pool ------------------------------
+//
+// Pass A traces a tile's segment trees without their shadow rays.  Its segments need no order
+// (each event links into its pixel's tree, trt_device.h), so the wave's lanes share their
+// pending segments: a lane that has finished its own work takes one from a LIFO pool of pending
+// refraction children in LDS (wave-aggregated, one rank per idle lane), and a lane that makes
+// two children continues with the reflection child and puts the other into the pool.  A deep
+// glass pixel's tree is spread over every lane of its wave instead of keeping one lane busy
+// while the others idle (round 3: 19.6 of 64 lanes active in pass A of the shipped frame).
+// When the pool is full a child goes to the lane's private overflow stack (<= MAX_DEPTH - 1
+// entries: their depths increase from bottom to top).
+#ifndef TRT_DEFER_POOL
+#define TRT_DEFER_POOL 128
+#endif
+constexpr uint32_t kPool = TRT_DEFER_POOL;
+constexpr int kPoolFields = 10; // o.xyz, d.xyz, thr, depth, parent link, pixel
+constexpr int defer_pool_floats() { return (int)kPool * kPoolFields; }
+
+struct PSeg {
+    Seg s;
+    uint32_t link; // parent event slot << 1 | (1: refraction child), or kEvRoot
+    uint32_t pix;  // output pixel
+};
+
+// SoA [field][entry]: the lanes of one take / push touch consecutive entries (conflict-free).
+__device__ __forceinline__ void pool_put(lds_f32* P, uint32_t e, const PSeg& x) {
+    P[0 * kPool + e] = x.s.o.x;
+    P[1 * kPool + e] = x.s.o.y;
+    P[2 * kPool + e] = x.s.o.z;
+    P[3 * kPool + e] = x.s.d.x;
+    P[4 * kPool + e] = x.s.d.y;
+    P[5 * kPool + e] = x.s.d.z;
+    P[6 * kPool + e] = x.s.thr;
+    P[7 * kPool + e] = __int_as_float(x.s.depth);
+    P[8 * kPool + e] = __uint_as_float(x.link);
+    P[9 * kPool + e] = __uint_as_float(x.pix);
+}
+__device__ __forceinline__ PSeg pool_get(const lds_f32* P, uint32_t e) {
+    PSeg x;
+    x.s = Seg{mk(P[0 * kPool + e], P[1 * kPool + e], P[2 * kPool + e]),
+              mk(P[3 * kPool + e], P[4 * kPool + e], P[5 * kPool + e]), P[6 * kPool + e],
+              __float_as_int(P[7 * kPool + e])};
+    x.link = __float_as_uint(P[8 * kPool + e]);
+    x.pix = __float_as_uint(P[9 * kPool + e]);
+    return x;
+}
+
+// A pixel whose log does not fit (event pool, query queue or task queue full) is re-traced in
+// place by defer_fallback: its tree root becomes kEvNone and it is listed once.
+__device__ __forceinline__ void defer_mark_fallback(const KArgs& A, uint32_t pix) {
+    if (atomicExch(&A.px_ev[pix].x, kEvNone) != kEvNone) A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
+}
+
+// Pass A over the segments the wave's lanes start with (`have`: the lane holds `cur`, whose
+// event links to `link` of pixel `pix`) and everything they spawn.  Every lane of the wave
+// must call it (ballots, the shared pool); it returns when no lane holds work.
+template <int GEOM, bool SPLIT>
+__device__ __forceinline__ void defer_walk(const KArgs& A, float* lds, float4* slab, EvLog& L, bool have, Seg cur,
+                                           uint32_t link, uint32_t pix) {
+    const int D = (int)A.max_depth;
+    lds_f32* P = (lds_f32*)lds;
+    Cnt cnt;
+    PSeg priv[kMaxTreeDepth];
+    int pn = 0;
+    uint32_t pool_n = 0; // wave-uniform
+    for (;;) {
+        if (!have && pn > 0) {
+            --pn;
+            cur = priv[pn].s;
+            link = priv[pn].link;
+            pix = priv[pn].pix;
+            have = true;
+        }
+        const uint64_t idle = __ballot(!have);
+        if (idle != 0ull && pool_n != 0u) {
+            const uint32_t take = min((uint32_t)__popcll(idle), pool_n);
+            if (!have) {
+                const uint32_t r = lane_rank(idle);
+                if (r < take) {
+                    const PSeg x = pool_get(P, pool_n - 1u - r);
+                    cur = x.s;
+                    link = x.link;
+                    pix = x.pix;
+                    have = true;
+                }
+            }
+            pool_n -= take;
+        }
+        if (__ballot(have) == 0ull) break;
+        // every lane takes this step's slot, working or not: the lanes stay on one row of one
+        // chunk (one chunk per kEvRows steps of the wave, coalesced event stores); idle lanes'
+        // slots stay unused
+        const uint32_t slot = ev_alloc(A, L);
+        bool have_other = false;
+        PSeg other;
+        if (have) {
+            have = false;
+            if (L.ovf && link == kEvRoot) { // no event this frame yet: list the pixel
+                atomicExch(&A.px_ev[pix].x, kEvNone);
+                A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
+            } else if (L.ovf) {
+                defer_mark_fallback(A, pix);
+            } else {
+                // where this segment's event lives: the pixel's root, or its parent's child link
+                if (link == kEvRoot) atomicExch(&A.px_ev[pix].x, slot);
+                else reinterpret_cast<uint32_t*>(ev_plane(A, link >> 1, 3))[2u + (link & 1u)] = slot;
+                Hit h;
+                scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
+                if (h.kind == HIT_NONE) {
+                    const f3 c = muls(background(A, cur.d), cur.thr);
+                    *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst));
+                } else {
+                    const Surf s = resolve_hit<false>(A, cur, h, cnt);
+                    const f3 v = neg(cur.d);
+                    float dterm[3] = {0.0f, 0.0f, 0.0f}, sterm[3] = {0.0f, 0.0f, 0.0f};
+                    uint32_t qmask = 0; // lights whose shadow query went to A.shq
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const LightTerm t = light_term(A, s, v, i);
+                        if (!t.matters) continue;
+                        // append the query (lanes of one light together: neighbouring queries of
+                        // the dense pass-B queue share a light and nearby origins)
+                        const uint64_t m = __ballot(true);
+                        const int leader = __ffsll((unsigned long long)m) - 1;
+                        uint32_t base = 0;
+                        if ((int)lane_id() == leader)
+                            base = atomicAdd(&A.dctr->nq[L.stripe * kCtrStride], (uint32_t)__popcll(m));
+                        base = __shfl(base, leader, 64);
+                        const uint32_t qi = base + lane_rank(m);
+                        if (qi < A.shq_cap) {
+                            float4* q = A.shq + 2 * ((size_t)L.stripe * A.shq_cap + qi);
+                            q[0] = make_float4(t.so.x, t.so.y, t.so.z, t.dist);
+                            q[1] = make_float4(t.ld.x, t.ld.y, t.ld.z, __uint_as_float((slot << 2) | (uint32_t)i));
+                            qmask |= 1u << i;
+                            dterm[i] = t.diff;
+                            sterm[i] = t.spec;
+                        } else {
+                            L.ovf = true;
+                        }
+                    }
+                    bool mk_refr, mk_refl;
+                    Seg refr, refl;
+                    make_children(cur, s, D, refr, mk_refr, refl, mk_refl);
+                    const uint32_t lrefl = slot << 1, lrefr = (slot << 1) | 1u;
+                    const uint32_t kids = (mk_refl ? kEvTagRefl : 0u) | (mk_refr ? kEvTagRefr : 0u);
+                    if (SPLIT && cur.depth + 1 >= (int)A.split_d1 && !L.ovf) {
+                        // window edge: both children become tasks of the next round
+                        bool sa = mk_refl, sb = mk_refr;
+                        enqueue2<true>(A, sa, refl, sb, refr, pix, lrefl, lrefr);
+                        if (sa != mk_refl || sb != mk_refr) L.ovf = true; // task queue full
+                        mk_refl = mk_refr = false;
+                    }
+                    if (L.ovf) {
+                        defer_mark_fallback(A, pix);
+                    } else {
+                        if (qmask == 0u) { // no light can add anything: the colour term is known now
+                            f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
+                            const f3 c = muls(add(muls(diffuse, s.alb[0]), muls(specular, s.alb[1])), cur.thr);
+                            *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst | kids));
+                        } else { // pass B ORs the occluded lights into plane 3's second word
+                            *ev_plane(A, slot, 0) = make_float4(s.kd[0], s.kd[1], s.kd[2], __uint_as_float(qmask | kids));
+                            *ev_plane(A, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], s.alb[0]);
+                            *ev_plane(A, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], s.alb[1]);
+                            *reinterpret_cast<float2*>(ev_plane(A, slot, 3)) = make_float2(cur.thr, 0.0f);
+                        }
+                        // continue with the reflection child (the reference pops it first; here
+                        // it keeps the lane on nearby rays), offer the refraction child to the wave
+                        if (mk_refl) {
+                            if (mk_refr) {
+                                other = PSeg{refr, lrefr, pix};
+                                have_other = true;
+                            }
+                            cur = refl;
+                            link = lrefl;
+                            have = true;
+                        } else if (mk_refr) {
+                            cur = refr;
+                            link = lrefr;
+                            have = true;
+                        }
+                    }
+                }
+            }
+        }
+        const uint64_t pm = __ballot(have_other);
+        if (pm != 0ull) {
+            const uint32_t room = kPool - pool_n;
+            wave_lds_sync(); // this step's takes have read the entries the pushes may reuse
+            if (have_other) {
+                const uint32_t r = lane_rank(pm);
+                if (r < room) pool_put(P, pool_n + r, other);
+                else priv[pn++] = other;
+            }
+            pool_n += min((uint32_t)__popcll(pm), room);
+            wave_lds_sync(); // the pushes land before the next step's takes
+        }
+    }
 }
 
 template <int CAP, bool COUNT, int GEOM>
@@ -1902,35 +2148,26 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
+    if constexpr (DEFER) { // pass A of a deferred-shadow frame (spp == 1): every lane walks
+        const bool valid = x < A.width && k < A.rows;
+        EvLog L;
+        // multiplicative hash of the tile: a frame's costly region (a glass object) spans few
+        // tile columns, so tile % stripes would pile its queries into a few stripes
+        L.stripe = (tile * 0x9E3779B1u) >> (32 - 7);
+        static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
+        const size_t o = valid ? (size_t)k * A.width + x : 0u;
+        const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
+        defer_walk<GEOM, SPLIT>(A, lds, slab, L, valid, root, kEvRoot, (uint32_t)o);
+        return;
+    }
     if (x >= A.width || k >= A.rows) return;
 #ifdef TRT_DIAG_TRIVIAL
     if (F.out8) F.out8[(size_t)k * A.width + x] = 0xff000000u | x; // diagnostic: launch + store only
     return;
 #endif
     const uint32_t y = band_row(A, k);
-    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
     const size_t o = (size_t)k * A.width + x;
-    if (DEFER) { // pass A of a deferred-shadow frame (spp == 1)
-        EvLog L;
-        // multiplicative hash of the tile: a frame's costly region (a glass object) spans few
-        // tile columns, so tile % stripes would pile its queries into a few stripes
-        L.stripe = (tile * 0x9E3779B1u) >> (32 - 7);
-        static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
-        bool unused = false;
-        cast_seg<CAP, COUNT, GEOM, SPLIT, true, HYB>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds, slab,
-                                                     (uint32_t)o, unused, &L);
-        cnt.pri += 1;
-        A.px_ev[o] = make_uint2(L.ovf ? kEvNone : L.first, L.k);
-        const uint64_t fm = __ballot(L.ovf);
-        if (fm) {
-            const int leader = __ffsll((unsigned long long)fm) - 1;
-            uint32_t base = 0;
-            if ((int)lane == leader) base = atomicAdd(&A.dctr->nfb, (uint32_t)__popcll(fm));
-            base = __shfl(base, leader, 64);
-            if (L.ovf) A.fb[base + lane_rank(fm)] = (uint32_t)o;
-        }
-        return;
-    }
     if (SPLIT) {
         bool spilled = false;
         const f3 c = cast_seg<CAP, COUNT, GEOM, true>(A, Seg{orig, primary_dir(A, x, y, 0), 1.0f, 0}, cnt, lds,
@@ -2084,15 +2321,15 @@ __global__ __launch_bounds__(64 * TRT_WPB, (waves_per_simd<GEOM, ((SPLIT || DEFE
 #if TRT_WPB > 1
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
     // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
-    __shared__ float lds_all[lds_stack_floats<CAP>() * TRT_WPB];
+    __shared__ float lds_all[(DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()) * TRT_WPB];
     __shared__ float4 slab_all[slab_float4s<GEOM>() * TRT_WPB];
     const uint32_t w = threadIdx.x >> 6;
-    float* lds = lds_all + w * lds_stack_floats<CAP>();
+    float* lds = lds_all + w * (DEFER ? defer_pool_floats() : lds_stack_floats<CAP>());
     float4* slab = slab_all + w * slab_float4s<GEOM>();
     const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
     if (vb >= A.ntiles) return;
 #else
-    __shared__ float lds[lds_stack_floats<CAP>()];
+    __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()];
     // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
     __shared__ float4 slab[slab_float4s<GEOM>()];
     const uint32_t vb = blockIdx.x;
@@ -2192,12 +2429,12 @@ __global__ __launch_bounds__(64 * TRT_WPB, (waves_per_simd<GEOM, ((SPLIT || DEFE
 // window-edge children go to the next queue) and add the subtree's colour to its pixel's
 // fixed-point sum.  Every wave leaves once the queue is drained.
 //
-// DEFER: a task logs its subtree's events into a chain of its own and writes the chain's head
-// into the LINK event its parent logged; a task whose log does not fit hands its pixel to
-// defer_fallback (the pixel's whole tree is re-traced; its other chains are then unused).
+// DEFER: a task is a segment of some pixel's tree whose event links into its parent's (the
+// link its parent queued with it); the wave's 64 tasks and their subtrees share the wave's
+// segment pool (defer_walk).
 template <int CAP, bool COUNT, int GEOM, bool DEFER = false>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs A) {
-    __shared__ float lds[lds_stack_floats<CAP>()];
+    __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = min(*A.q_in_n, A.q_cap);
@@ -2205,6 +2442,24 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
     // on one device-scope counter cost ~4x the tasks' own work: profiles/r02_ab_tasks_static.log)
     for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
         const uint32_t t = base + threadIdx.x;
+        if constexpr (DEFER) {
+            const bool valid = t < n;
+            Seg root{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f), 0.0f, 0};
+            uint32_t pixel = 0, link = kEvRoot;
+            if (valid) {
+                const float4* q = reinterpret_cast<const float4*>(A.q_in + t);
+                const float4 a = q[0], b = q[1];
+                const uint32_t pd = __float_as_uint(b.w);
+                pixel = pd >> kTaskDepthBits;
+                root = Seg{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z, (int)(pd & ((1u << kTaskDepthBits) - 1u))};
+                link = A.q_link_in[t];
+            }
+            EvLog L;
+            // wave-uniform (ev_alloc and the query appends reserve from one stripe per wave)
+            L.stripe = ((base / 64u + 0x5bd1e995u * A.split_d1) * 0x9E3779B1u) >> (32 - 7);
+            defer_walk<GEOM, true>(A, lds, slab, L, valid, root, link, pixel);
+            continue;
+        }
         if (t < n) {
             const float4* q = reinterpret_cast<const float4*>(A.q_in + t);
             const float4 a = q[0], b = q[1];
@@ -2212,19 +2467,6 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
             const uint32_t pixel = pd >> kTaskDepthBits;
             const Seg root{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), b.z, (int)(pd & ((1u << kTaskDepthBits) - 1u))};
             bool spilled = false;
-            if (DEFER) {
-                EvLog L;
-                // wave-uniform (ev_alloc and the query appends reserve from the stripe of the
-                // wave's leader for every lane of the wave)
-                L.stripe = ((base / 64u + 0x5bd1e995u * A.split_d1) * 0x9E3779B1u) >> (32 - 7);
-                cast_seg<CAP, false, GEOM, true, true, true>(A, root, cnt, lds, slab, pixel, spilled, &L);
-                *ev_plane(A, A.q_link_in[t], 0) = make_float4(__uint_as_float(L.first), __uint_as_float(L.k),
-                                                              __uint_as_float(lane_id()), __uint_as_float(kEvLink));
-                // the first chain of a pixel to overflow lists it (pass A lists its own)
-                if (L.ovf && atomicExch(reinterpret_cast<uint32_t*>(A.px_ev + pixel), kEvNone) != kEvNone)
-                    A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pixel;
-                continue;
-            }
             const f3 c = cast_seg<CAP, COUNT, GEOM, true>(A, root, cnt, lds, slab, pixel, spilled);
             unsigned long long* acc = A.acc + 4 * (size_t)pixel;
             atomicAdd(acc + 0, to_fixed(c.x));
@@ -2296,67 +2538,62 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArg
     }
 }
 
-// Pass C: each pixel's events summed in the order its DFS logged them — the reference's pop
-// order — with exactly cast_seg's arithmetic (a lit light's kd * diffuse / kd * specular terms
-// added in light order, then colour += thr * (diffuse * albedo.x + specular * albedo.y)); then
-// clamp, gamma and the dual store.  Lane = the pixel's lane in its pass-A tile.
+// Pass C: each pixel's event tree summed in the reference's pop order (shader.comp:530-575:
+// a segment, then its reflection subtree, then its refraction subtree) with exactly cast_seg's
+// arithmetic (a lit light's kd * diffuse / kd * specular terms added in light order, then
+// colour += thr * (diffuse * albedo.x + specular * albedo.y)); then clamp, gamma and the dual
+// store.  Lane = the pixel's lane in its pass-A tile.
 __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
     const uint32_t tile = blockIdx.x, lane = threadIdx.x;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;
     const size_t o = (size_t)k * A.width + x;
-    const uint2 pe = A.px_ev[o];
-    if (pe.x == kEvNone) return; // defer_fallback's pixel
+    const uint32_t root = A.px_ev[o].x;
+    if (root == kEvNone) return; // defer_fallback's pixel
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    // the chain being read: (chunk, lane column, next event, events); LINK events descend into
-    // a subtree's chain (split frames), its end returns to the parent's
-    uint32_t chunk = pe.x, col = lane, j = 0, n = pe.y, sp = 0, steps = 0;
-    uint4 stk[kMaxLinkDepth];
+    uint32_t stk[kMaxTreeDepth]; // pending refraction subtrees, one per depth of the path
+    uint32_t s = root, sp = 0, steps = 0;
     for (;;) {
-        if (++steps > 65536u) { // a corrupt log must not hang the GPU: flag it, paint the pixel
+        // a tree has at most 2^MAX_DEPTH - 1 events: a corrupt log must not hang the GPU
+        if (++steps > (1u << kMaxTreeDepth) || s >= A.ev_cap * kDeferStripes * kEvRows * 64u) {
             if (atomicCAS(&A.dctr->pad[0], 0u, 1u) == 0u) {
                 uint32_t* d = A.dctr->pad;
-                d[1] = (uint32_t)o; d[2] = pe.x; d[3] = pe.y; d[4] = chunk; d[5] = col; d[6] = j; d[7] = n; d[8] = sp;
-                for (uint32_t q = 0; q < sp && q < 2u; ++q) { d[9 + 3 * q] = stk[q].x; d[10 + 3 * q] = stk[q].z; d[11 + 3 * q] = stk[q].w; }
+                d[1] = (uint32_t)o; d[2] = root; d[3] = s; d[4] = sp; d[5] = steps;
             }
             color = mk(1.0f, 0.0f, 1.0f);
             break;
         }
-        if (j == n) {
-            if (sp == 0u) break;
-            const uint4 f = stk[--sp];
-            chunk = f.x, col = f.y, j = f.z, n = f.w;
-            continue;
-        }
-        const uint32_t row = j % kEvRows;
-        if (j != 0u && row == 0u) chunk = A.ev_next[(size_t)chunk * 64u + col];
-        ++j;
-        const uint32_t s = (chunk * kEvRows + row) * 64u + col;
         const float4 p0 = *ev_plane(A, s, 0);
         const uint32_t tag = __float_as_uint(p0.w);
-        if (tag == kEvConst) {
+        const float4 p3 = *ev_plane(A, s, 3);
+        if (tag & kEvTagConst) {
             color = add(color, mk(p0.x, p0.y, p0.z));
-            continue;
-        }
-        if (tag == kEvLink) {
-            if (sp < kMaxLinkDepth) stk[sp++] = make_uint4(chunk, col, j, n);
-            chunk = __float_as_uint(p0.x), col = __float_as_uint(p0.z), j = 0, n = __float_as_uint(p0.y);
-            continue;
-        }
-        const float4 p1 = *ev_plane(A, s, 1), p2 = *ev_plane(A, s, 2);
-        const float2 p3 = *reinterpret_cast<const float2*>(ev_plane(A, s, 3));
-        const uint32_t lit = tag & ~__float_as_uint(p3.y);
-        const f3 kdv = mk(p0.x, p0.y, p0.z);
-        const float dterm[3] = {p1.x, p1.y, p1.z}, sterm[3] = {p2.x, p2.y, p2.z};
-        f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
+        } else {
+            const float4 p1 = *ev_plane(A, s, 1), p2 = *ev_plane(A, s, 2);
+            const uint32_t lit = tag & 7u & ~__float_as_uint(p3.y);
+            const f3 kdv = mk(p0.x, p0.y, p0.z);
+            const float dterm[3] = {p1.x, p1.y, p1.z}, sterm[3] = {p2.x, p2.y, p2.z};
+            f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (!((lit >> i) & 1u)) continue;
-            diffuse = add(diffuse, muls(kdv, dterm[i]));
-            specular = add(specular, muls(kdv, sterm[i]));
+            for (int i = 0; i < 3; ++i) {
+                if (!((lit >> i) & 1u)) continue;
+                diffuse = add(diffuse, muls(kdv, dterm[i]));
+                specular = add(specular, muls(kdv, sterm[i]));
+            }
+            color = add(color, muls(add(muls(diffuse, p1.w), muls(specular, p2.w)), p3.x));
         }
-        color = add(color, muls(add(muls(diffuse, p1.w), muls(specular, p2.w)), p3.x));
+        const uint32_t refl = __float_as_uint(p3.z), refr = __float_as_uint(p3.w);
+        if (tag & kEvTagRefl) {
+            if ((tag & kEvTagRefr) && sp < kMaxTreeDepth) stk[sp++] = refr;
+            s = refl;
+        } else if (tag & kEvTagRefr) {
+            s = refr;
+        } else if (sp > 0u) {
+            s = stk[--sp];
+        } else {
+            break;
+        }
     }
     store_pixel(A, A.fr[0], o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
 }
@@ -2400,7 +2637,7 @@ static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
         A.q_out = A.q_buf[0];
         A.q_link_out = A.q_link_buf[0];
         A.q_out_n = &A.ctr->produced[0];
-        if (stages & 1) hipLaunchKernelGGL((trace_kernel<CAP, false, GEOM, true, true, true>), grid, block, 0, stream, A);
+        if (stages & 1) hipLaunchKernelGGL((trace_kernel<0, false, GEOM, true, true, false>), grid, block, 0, stream, A);
         uint32_t r = 1;
         for (uint32_t d0 = W; d0 < D && r <= kMaxSplitRounds && (stages & 2); d0 += W, ++r) {
             A.split_d1 = d0 + W;
@@ -2411,11 +2648,11 @@ static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
             A.q_out = A.q_buf[r & 1];
             A.q_link_out = A.q_link_buf[r & 1];
             A.q_out_n = &A.ctr->produced[r];
-            hipLaunchKernelGGL((trace_tasks<CAP, false, GEOM, true>), dim3(A.num_cus * (GEOM == 3 ? 4 * TRT_G3_WAVES : 12)),
+            hipLaunchKernelGGL((trace_tasks<0, false, GEOM, true>), dim3(A.num_cus * (GEOM == 3 ? 4 * TRT_G3_WAVES : 12)),
                                dim3(64), 0, stream, A);
         }
     } else {
-        hipLaunchKernelGGL((trace_kernel<CAP, false, GEOM, false, true, HYB>), grid, block, 0, stream, A);
+        hipLaunchKernelGGL((trace_kernel<0, false, GEOM, false, true, false>), grid, block, 0, stream, A);
     }
     // persistent: up to 8 waves per SIMD (the shadow-only kernel is light on VGPRs and LDS;
     // waves that find the queue drained exit at once)

@@ -251,7 +251,6 @@ int trt_destroy(trt_ctx* c) {
         (void)hipFree(b.spilled);
         (void)hipFree(b.ctr);
         (void)hipFree(b.ev);
-        (void)hipFree(b.ev_next);
         (void)hipFree(b.shq);
         (void)hipFree(b.px_ev);
         (void)hipFree(b.fb);
@@ -706,18 +705,15 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
                                              0xFFFFFFFFu / S);
     if (chunks > b.ev_chunks || qcap > b.shq_cap || npx > b.dnpx) {
         (void)hipFree(b.ev);
-        (void)hipFree(b.ev_next);
         (void)hipFree(b.shq);
         (void)hipFree(b.px_ev);
         (void)hipFree(b.fb);
         b.ev = nullptr;
-        b.ev_next = nullptr;
         b.shq = nullptr;
         b.px_ev = nullptr;
         b.fb = nullptr;
         b.ev_chunks = b.shq_cap = b.dnpx = 0;
         hipError_t e = hipMalloc((void**)&b.ev, chunks * trt::kEvRows * 4 * 64 * sizeof(float4));
-        if (e == hipSuccess) e = hipMalloc((void**)&b.ev_next, chunks * 64 * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMalloc((void**)&b.shq, qcap * 2 * sizeof(float4));
         if (e == hipSuccess) e = hipMalloc((void**)&b.px_ev, npx * sizeof(uint2));
         if (e == hipSuccess) e = hipMalloc((void**)&b.fb, npx * sizeof(uint32_t));
@@ -732,7 +728,6 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", b.ev_chunks / trt::kDeferStripes);
     A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", b.shq_cap / trt::kDeferStripes);
     A.ev = b.ev;
-    A.ev_next = b.ev_next;
     A.shq = b.shq;
     A.px_ev = b.px_ev;
     A.fb = b.fb;
