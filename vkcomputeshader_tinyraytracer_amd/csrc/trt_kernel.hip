@@ -520,10 +520,13 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
                                          float max_dist, float& best, Cnt& c) {
     const uint32_t first = node & kBvhFirstMask;
     const uint32_t n = ((node >> kBvhCountShift) & 15u) + 1u;
+#ifndef TRT_LEAF_PREFETCH
+#define TRT_LEAF_PREFETCH 1
+#endif
     TriGeo g = A.bvh_tris[first];
     for (uint32_t k = first; k < first + n; ++k) {
-        const TriGeo cur = g;
-        if (k + 1 < first + n) g = A.bvh_tris[k + 1];
+        const TriGeo cur = TRT_LEAF_PREFETCH ? g : A.bvh_tris[k];
+        if (TRT_LEAF_PREFETCH && k + 1 < first + n) g = A.bvh_tris[k + 1];
         if (COUNT) ++c.tt;
 #ifdef TRT_DIAG_PIXEL_WORK
         ++c.wt;
@@ -1265,6 +1268,46 @@ __device__ __forceinline__ float unorm8(uint32_t c) {
     return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
+// atan2 / acos for direction_to_uv as short polynomials (SLEEF's single-precision minimax
+// sets, a few ulp like ocml's; the oracle uses libm either way, tests/helpers.py FLOAT_TOL):
+// opt-in experiment, the envmap lookups of C2 price these (tools/r04_ab_c2.sh).
+#ifndef TRT_FAST_TRIG
+#define TRT_FAST_TRIG 0
+#endif
+__device__ __forceinline__ float atan2_poly(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float s = a * a;
+    float u = 0.00282363896258175373077393f;
+    u = __builtin_fmaf(u, s, -0.0159569028764963150024414f);
+    u = __builtin_fmaf(u, s, 0.0425049886107444763183594f);
+    u = __builtin_fmaf(u, s, -0.0748900920152664184570312f);
+    u = __builtin_fmaf(u, s, 0.106347933411598205566406f);
+    u = __builtin_fmaf(u, s, -0.142027363181114196777344f);
+    u = __builtin_fmaf(u, s, 0.199926957488059997558594f);
+    u = __builtin_fmaf(u, s, -0.333331018686294555664062f);
+    float r = __builtin_fmaf(s * a, u, a);
+    r = ay > ax ? 1.57079632679489661923f - r : r;
+    r = x < 0.0f ? 3.14159265358979323846f - r : r;
+    return __builtin_copysignf(r, y);
+}
+__device__ __forceinline__ float acos_poly(float d) {
+    const float ad = fabsf(d);
+    const bool o = ad < 0.5f;
+    const float x2 = o ? d * d : (1.0f - ad) * 0.5f;
+    float x = o ? ad : __builtin_sqrtf(x2);
+    float u = 0.4197454825e-1f;
+    u = __builtin_fmaf(u, x2, 0.2424046025e-1f);
+    u = __builtin_fmaf(u, x2, 0.4547423869e-1f);
+    u = __builtin_fmaf(u, x2, 0.7495029271e-1f);
+    u = __builtin_fmaf(u, x2, 0.1666677296e+0f);
+    u *= x * x2;
+    if (o) return 1.57079632679489661923f - (__builtin_copysignf(x, d) + __builtin_copysignf(u, d));
+    const float r = 2.0f * (x + u);
+    return d < 0.0f ? 3.14159265358979323846f - r : r;
+}
+
 #ifndef TRT_ENV_PAIRROWS
 #define TRT_ENV_PAIRROWS 1
 #endif
@@ -1288,6 +1331,9 @@ __device__ __forceinline__ EnvFetch env_fetch(const KArgs& A, f3 d) {
 #ifdef TRT_DIAG_NO_UV_TRIG
     // diagnostic: prices atan2 / acos (wrong texels, same memory pattern class)
     float theta = d.z * 3.0f, phi = (d.y + 1.0f) * 1.5f;
+#elif TRT_FAST_TRIG
+    float theta = atan2_poly(d.z, d.x);
+    float phi = acos_poly(fminf(fmaxf(d.y, -1.0f), 1.0f));
 #else
     float theta = atan2f(d.z, d.x);
     float phi = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
@@ -2701,6 +2747,14 @@ hipError_t launch_shadow_batch(const KArgs& A0, const float4* rays, uint32_t n, 
 // split window of w depths at most w - 1 do, so split launches keep w - 1 in LDS).  With a
 // split window (A.split_w in [2, 5], spp == 1, max_depth > window) the frame is traced in
 // depth windows: the tile kernel, one trace_tasks round per further window, finalize_spilled.
+#ifdef TRT_KRES_ONLY
+// tools/kres_quick.sh: compile only the kernels named by TRT_KRES_ONLY (register studies in a
+// fraction of the full build's time; the library is not linkable from this object)
+hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool) {
+    hipLaunchKernelGGL((TRT_KRES_ONLY), dim3(1), dim3(64), 0, stream, A);
+    return hipGetLastError();
+}
+#else
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const uint32_t D = A.max_depth;
 #if defined(TRT_PERSIST)
@@ -2790,6 +2844,7 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
 #undef TRT_LAUNCH_G
     return hipGetLastError();
 }
+#endif
 
 } // namespace trt
 
