@@ -91,7 +91,6 @@ for v in "$@"; do
         bgearly_wpb4) variant bgearly_wpb4 -DTRT_BG_EARLY -DTRT_WPB=4 ;;
         notrig) variant notrig -DTRT_DIAG_NO_UV_TRIG ;;
         pool64) variant pool64 -DTRT_DEFER_POOL=64 ;;
-        fasttrig) variant fasttrig -DTRT_FAST_TRIG=1 ;;
         pool192) variant pool192 -DTRT_DEFER_POOL=192 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac

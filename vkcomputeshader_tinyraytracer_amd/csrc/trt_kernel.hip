@@ -1268,46 +1268,6 @@ __device__ __forceinline__ float unorm8(uint32_t c) {
     return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, x), r, q);
 }
 
-// atan2 / acos for direction_to_uv as short polynomials (SLEEF's single-precision minimax
-// sets, a few ulp like ocml's; the oracle uses libm either way, tests/helpers.py FLOAT_TOL):
-// opt-in experiment, the envmap lookups of C2 price these (tools/r04_ab_c2.sh).
-#ifndef TRT_FAST_TRIG
-#define TRT_FAST_TRIG 0
-#endif
-__device__ __forceinline__ float atan2_poly(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
-    const float s = a * a;
-    float u = 0.00282363896258175373077393f;
-    u = __builtin_fmaf(u, s, -0.0159569028764963150024414f);
-    u = __builtin_fmaf(u, s, 0.0425049886107444763183594f);
-    u = __builtin_fmaf(u, s, -0.0748900920152664184570312f);
-    u = __builtin_fmaf(u, s, 0.106347933411598205566406f);
-    u = __builtin_fmaf(u, s, -0.142027363181114196777344f);
-    u = __builtin_fmaf(u, s, 0.199926957488059997558594f);
-    u = __builtin_fmaf(u, s, -0.333331018686294555664062f);
-    float r = __builtin_fmaf(s * a, u, a);
-    r = ay > ax ? 1.57079632679489661923f - r : r;
-    r = x < 0.0f ? 3.14159265358979323846f - r : r;
-    return __builtin_copysignf(r, y);
-}
-__device__ __forceinline__ float acos_poly(float d) {
-    const float ad = fabsf(d);
-    const bool o = ad < 0.5f;
-    const float x2 = o ? d * d : (1.0f - ad) * 0.5f;
-    float x = o ? ad : __builtin_sqrtf(x2);
-    float u = 0.4197454825e-1f;
-    u = __builtin_fmaf(u, x2, 0.2424046025e-1f);
-    u = __builtin_fmaf(u, x2, 0.4547423869e-1f);
-    u = __builtin_fmaf(u, x2, 0.7495029271e-1f);
-    u = __builtin_fmaf(u, x2, 0.1666677296e+0f);
-    u *= x * x2;
-    if (o) return 1.57079632679489661923f - (__builtin_copysignf(x, d) + __builtin_copysignf(u, d));
-    const float r = 2.0f * (x + u);
-    return d < 0.0f ? 3.14159265358979323846f - r : r;
-}
-
 #ifndef TRT_ENV_PAIRROWS
 #define TRT_ENV_PAIRROWS 1
 #endif
@@ -1329,11 +1289,10 @@ __device__ __forceinline__ EnvFetch env_fetch(const KArgs& A, f3 d) {
     }
 #endif
 #ifdef TRT_DIAG_NO_UV_TRIG
-    // diagnostic: prices atan2 / acos (wrong texels, same memory pattern class)
+    // diagnostic: prices atan2 / acos (wrong texels): C2 13.85 -> 13.23 us per frame; SLEEF-style
+    // minimax polynomials in their place measured 13.95 (profiles/r04c_ab_c2_stages.jsonl), so
+    // ocml's stay
     float theta = d.z * 3.0f, phi = (d.y + 1.0f) * 1.5f;
-#elif TRT_FAST_TRIG
-    float theta = atan2_poly(d.z, d.x);
-    float phi = acos_poly(fminf(fmaxf(d.y, -1.0f), 1.0f));
 #else
     float theta = atan2f(d.z, d.x);
     float phi = acosf(fminf(fmaxf(d.y, -1.0f), 1.0f));
