@@ -91,6 +91,11 @@ for v in "$@"; do
         bgearly_wpb4) variant bgearly_wpb4 -DTRT_BG_EARLY -DTRT_WPB=4 ;;
         notrig) variant notrig -DTRT_DIAG_NO_UV_TRIG ;;
         pool64) variant pool64 -DTRT_DEFER_POOL=64 ;;
+        norefill) variant norefill -DTRT_DEFER_REFILL=0 ;;
+        t16) variant t16 -DTRT_REFILL_T=16 ;;
+        t48) variant t48 -DTRT_REFILL_T=48 ;;
+        t56) variant t56 -DTRT_REFILL_T=56 ;;
+        srefill) variant srefill -DTRT_SHADOW_REFILL=1 ;;
         pool192) variant pool192 -DTRT_DEFER_POOL=192 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac

@@ -1908,41 +1908,163 @@ __device__ __forceinline__ void defer_mark_fallback(const KArgs& A, uint32_t pix
     if (atomicExch(&A.px_ev[pix].x, kEvNone) != kEvNone) A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
 }
 
+// One traced segment of pass A: its event (slot `slot`, linked to `link` of pixel `pix`), its
+// shadow queries and its children.  `h` is the segment's closest hit (unused when the event
+// pool overflowed).  On return `have` says whether the lane continues with a child (then in
+// `cur` / `link`), and `have_other` whether it offers a second child to the wave.
+template <bool SPLIT>
+__device__ __forceinline__ void defer_shade(const KArgs& A, EvLog& L, uint32_t slot, const Hit& h, Seg& cur,
+                                            uint32_t& link, uint32_t pix, bool& have, PSeg& other, bool& have_other) {
+    const int D = (int)A.max_depth;
+    Cnt cnt;
+    have = false;
+    if (L.ovf && link == kEvRoot) { // no event this frame yet: list the pixel
+        atomicExch(&A.px_ev[pix].x, kEvNone);
+        A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
+        return;
+    }
+    if (L.ovf) {
+        defer_mark_fallback(A, pix);
+        return;
+    }
+    // where this segment's event lives: the pixel's root, or its parent's child link
+    if (link == kEvRoot) atomicExch(&A.px_ev[pix].x, slot);
+    else reinterpret_cast<uint32_t*>(ev_plane(A, link >> 1, 3))[2u + (link & 1u)] = slot;
+    if (h.kind == HIT_NONE) {
+        const f3 c = muls(background(A, cur.d), cur.thr);
+        *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst));
+        return;
+    }
+    const Surf s = resolve_hit<false>(A, cur, h, cnt);
+    const f3 v = neg(cur.d);
+    float dterm[3] = {0.0f, 0.0f, 0.0f}, sterm[3] = {0.0f, 0.0f, 0.0f};
+    uint32_t qmask = 0; // lights whose shadow query went to A.shq
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const LightTerm t = light_term(A, s, v, i);
+        if (!t.matters) continue;
+        // append the query (lanes of one light together: neighbouring queries of the dense
+        // pass-B queue share a light and nearby origins)
+        const uint64_t m = __ballot(true);
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if ((int)lane_id() == leader) base = atomicAdd(&A.dctr->nq[L.stripe * kCtrStride], (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        const uint32_t qi = base + lane_rank(m);
+        if (qi < A.shq_cap) {
+            float4* q = A.shq + 2 * ((size_t)L.stripe * A.shq_cap + qi);
+            q[0] = make_float4(t.so.x, t.so.y, t.so.z, t.dist);
+            q[1] = make_float4(t.ld.x, t.ld.y, t.ld.z, __uint_as_float((slot << 2) | (uint32_t)i));
+            qmask |= 1u << i;
+            dterm[i] = t.diff;
+            sterm[i] = t.spec;
+        } else {
+            L.ovf = true;
+        }
+    }
+    bool mk_refr, mk_refl;
+    Seg refr, refl;
+    make_children(cur, s, D, refr, mk_refr, refl, mk_refl);
+    const uint32_t lrefl = slot << 1, lrefr = (slot << 1) | 1u;
+    const uint32_t kids = (mk_refl ? kEvTagRefl : 0u) | (mk_refr ? kEvTagRefr : 0u);
+    if (SPLIT && cur.depth + 1 >= (int)A.split_d1 && !L.ovf) {
+        // window edge: both children become tasks of the next round
+        bool sa = mk_refl, sb = mk_refr;
+        enqueue2<true>(A, sa, refl, sb, refr, pix, lrefl, lrefr);
+        if (sa != mk_refl || sb != mk_refr) L.ovf = true; // task queue full
+        mk_refl = mk_refr = false;
+    }
+    if (L.ovf) {
+        defer_mark_fallback(A, pix);
+        return;
+    }
+    if (qmask == 0u) { // no light can add anything: the colour term is known now
+        f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
+        const f3 c = muls(add(muls(diffuse, s.alb[0]), muls(specular, s.alb[1])), cur.thr);
+        *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst | kids));
+    } else { // pass B ORs the occluded lights into plane 3's second word
+        *ev_plane(A, slot, 0) = make_float4(s.kd[0], s.kd[1], s.kd[2], __uint_as_float(qmask | kids));
+        *ev_plane(A, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], s.alb[0]);
+        *ev_plane(A, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], s.alb[1]);
+        *reinterpret_cast<float2*>(ev_plane(A, slot, 3)) = make_float2(cur.thr, 0.0f);
+    }
+    // continue with the reflection child (the reference pops it first; here it keeps the lane
+    // on nearby rays), offer the refraction child to the wave
+    if (mk_refl) {
+        if (mk_refr) {
+            other = PSeg{refr, lrefr, pix};
+            have_other = true;
+        }
+        cur = refl;
+        link = lrefl;
+        have = true;
+    } else if (mk_refr) {
+        cur = refr;
+        link = lrefr;
+        have = true;
+    }
+}
+
+// The wave's pending-segment pool (defer_walk / defer_walk_q): a lane without work takes its
+// private overflow first, then the pool's top entries (wave-aggregated, one per idle lane by
+// rank); `want` lanes get work.  pool_n is wave-uniform.
+__device__ __forceinline__ void pool_refill(const lds_f32* P, uint32_t& pool_n, PSeg* priv, int& pn, bool want,
+                                            bool& got, Seg& cur, uint32_t& link, uint32_t& pix) {
+    got = false;
+    if (want && pn > 0) {
+        --pn;
+        cur = priv[pn].s;
+        link = priv[pn].link;
+        pix = priv[pn].pix;
+        got = true;
+    }
+    const uint64_t idle = __ballot(want && !got);
+    if (idle != 0ull && pool_n != 0u) {
+        const uint32_t take = min((uint32_t)__popcll(idle), pool_n);
+        if (want && !got) {
+            const uint32_t r = lane_rank(idle);
+            if (r < take) {
+                const PSeg x = pool_get(P, pool_n - 1u - r);
+                cur = x.s;
+                link = x.link;
+                pix = x.pix;
+                got = true;
+            }
+        }
+        pool_n -= take;
+    }
+}
+// Lanes with a second child put it into the pool (or their private overflow when it is full).
+__device__ __forceinline__ void pool_offer(lds_f32* P, uint32_t& pool_n, PSeg* priv, int& pn, bool have_other,
+                                           const PSeg& other) {
+    const uint64_t pm = __ballot(have_other);
+    if (pm == 0ull) return;
+    const uint32_t room = kPool - pool_n;
+    wave_lds_sync(); // this step's takes have read the entries the pushes may reuse
+    if (have_other) {
+        const uint32_t r = lane_rank(pm);
+        if (r < room) pool_put(P, pool_n + r, other);
+        else priv[pn++] = other;
+    }
+    pool_n += min((uint32_t)__popcll(pm), room);
+    wave_lds_sync(); // the pushes land before the next step's takes
+}
+
 // Pass A over the segments the wave's lanes start with (`have`: the lane holds `cur`, whose
 // event links to `link` of pixel `pix`) and everything they spawn.  Every lane of the wave
 // must call it (ballots, the shared pool); it returns when no lane holds work.
 template <int GEOM, bool SPLIT>
 __device__ __forceinline__ void defer_walk(const KArgs& A, float* lds, float4* slab, EvLog& L, bool have, Seg cur,
                                            uint32_t link, uint32_t pix) {
-    const int D = (int)A.max_depth;
     lds_f32* P = (lds_f32*)lds;
     Cnt cnt;
     PSeg priv[kMaxTreeDepth];
     int pn = 0;
     uint32_t pool_n = 0; // wave-uniform
     for (;;) {
-        if (!have && pn > 0) {
-            --pn;
-            cur = priv[pn].s;
-            link = priv[pn].link;
-            pix = priv[pn].pix;
-            have = true;
-        }
-        const uint64_t idle = __ballot(!have);
-        if (idle != 0ull && pool_n != 0u) {
-            const uint32_t take = min((uint32_t)__popcll(idle), pool_n);
-            if (!have) {
-                const uint32_t r = lane_rank(idle);
-                if (r < take) {
-                    const PSeg x = pool_get(P, pool_n - 1u - r);
-                    cur = x.s;
-                    link = x.link;
-                    pix = x.pix;
-                    have = true;
-                }
-            }
-            pool_n -= take;
-        }
+        bool got;
+        pool_refill(P, pool_n, priv, pn, !have, got, cur, link, pix);
+        have = have || got;
         if (__ballot(have) == 0ull) break;
         // every lane takes this step's slot, working or not: the lanes stay on one row of one
         // chunk (one chunk per kEvRows steps of the wave, coalesced event stores); idle lanes'
@@ -1951,105 +2073,150 @@ __device__ __forceinline__ void defer_walk(const KArgs& A, float* lds, float4* s
         bool have_other = false;
         PSeg other;
         if (have) {
-            have = false;
-            if (L.ovf && link == kEvRoot) { // no event this frame yet: list the pixel
-                atomicExch(&A.px_ev[pix].x, kEvNone);
-                A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
-            } else if (L.ovf) {
-                defer_mark_fallback(A, pix);
-            } else {
-                // where this segment's event lives: the pixel's root, or its parent's child link
-                if (link == kEvRoot) atomicExch(&A.px_ev[pix].x, slot);
-                else reinterpret_cast<uint32_t*>(ev_plane(A, link >> 1, 3))[2u + (link & 1u)] = slot;
-                Hit h;
-                scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
-                if (h.kind == HIT_NONE) {
-                    const f3 c = muls(background(A, cur.d), cur.thr);
-                    *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst));
-                } else {
-                    const Surf s = resolve_hit<false>(A, cur, h, cnt);
-                    const f3 v = neg(cur.d);
-                    float dterm[3] = {0.0f, 0.0f, 0.0f}, sterm[3] = {0.0f, 0.0f, 0.0f};
-                    uint32_t qmask = 0; // lights whose shadow query went to A.shq
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const LightTerm t = light_term(A, s, v, i);
-                        if (!t.matters) continue;
-                        // append the query (lanes of one light together: neighbouring queries of
-                        // the dense pass-B queue share a light and nearby origins)
-                        const uint64_t m = __ballot(true);
-                        const int leader = __ffsll((unsigned long long)m) - 1;
-                        uint32_t base = 0;
-                        if ((int)lane_id() == leader)
-                            base = atomicAdd(&A.dctr->nq[L.stripe * kCtrStride], (uint32_t)__popcll(m));
-                        base = __shfl(base, leader, 64);
-                        const uint32_t qi = base + lane_rank(m);
-                        if (qi < A.shq_cap) {
-                            float4* q = A.shq + 2 * ((size_t)L.stripe * A.shq_cap + qi);
-                            q[0] = make_float4(t.so.x, t.so.y, t.so.z, t.dist);
-                            q[1] = make_float4(t.ld.x, t.ld.y, t.ld.z, __uint_as_float((slot << 2) | (uint32_t)i));
-                            qmask |= 1u << i;
-                            dterm[i] = t.diff;
-                            sterm[i] = t.spec;
-                        } else {
-                            L.ovf = true;
-                        }
-                    }
-                    bool mk_refr, mk_refl;
-                    Seg refr, refl;
-                    make_children(cur, s, D, refr, mk_refr, refl, mk_refl);
-                    const uint32_t lrefl = slot << 1, lrefr = (slot << 1) | 1u;
-                    const uint32_t kids = (mk_refl ? kEvTagRefl : 0u) | (mk_refr ? kEvTagRefr : 0u);
-                    if (SPLIT && cur.depth + 1 >= (int)A.split_d1 && !L.ovf) {
-                        // window edge: both children become tasks of the next round
-                        bool sa = mk_refl, sb = mk_refr;
-                        enqueue2<true>(A, sa, refl, sb, refr, pix, lrefl, lrefr);
-                        if (sa != mk_refl || sb != mk_refr) L.ovf = true; // task queue full
-                        mk_refl = mk_refr = false;
-                    }
-                    if (L.ovf) {
-                        defer_mark_fallback(A, pix);
-                    } else {
-                        if (qmask == 0u) { // no light can add anything: the colour term is known now
-                            f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
-                            const f3 c = muls(add(muls(diffuse, s.alb[0]), muls(specular, s.alb[1])), cur.thr);
-                            *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst | kids));
-                        } else { // pass B ORs the occluded lights into plane 3's second word
-                            *ev_plane(A, slot, 0) = make_float4(s.kd[0], s.kd[1], s.kd[2], __uint_as_float(qmask | kids));
-                            *ev_plane(A, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], s.alb[0]);
-                            *ev_plane(A, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], s.alb[1]);
-                            *reinterpret_cast<float2*>(ev_plane(A, slot, 3)) = make_float2(cur.thr, 0.0f);
-                        }
-                        // continue with the reflection child (the reference pops it first; here
-                        // it keeps the lane on nearby rays), offer the refraction child to the wave
-                        if (mk_refl) {
-                            if (mk_refr) {
-                                other = PSeg{refr, lrefr, pix};
-                                have_other = true;
-                            }
-                            cur = refl;
-                            link = lrefl;
-                            have = true;
-                        } else if (mk_refr) {
-                            cur = refr;
-                            link = lrefr;
-                            have = true;
+            Hit h;
+            h.kind = HIT_NONE;
+            if (!L.ovf) scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
+            defer_shade<SPLIT>(A, L, slot, h, cur, link, pix, have, other, have_other);
+        }
+        pool_offer(P, pool_n, priv, pn, have_other, other);
+    }
+}
+
+// Pass A with the quantized BVH4 walk turned inside out (GEOM 3): the wave advances every
+// traversing lane by ONE node visit or leaf test per step, and a lane whose walk has ended
+// waits until fewer than TRT_REFILL_T lanes still walk; then the finished lanes are shaded
+// together (their events, queries and children) and refilled with new segments (their
+// reflection child, their private overflow, the wave's pool), so a wave no longer runs each
+// step as long as its longest walk (Aila & Laine's dynamic ray fetch).  The walk is
+// trace_bvh4's, visit for visit: the same closest hit.
+// Measured and rejected (round 4, profiles/r04d_ab_deep.jsonl): the shipped frame 442 -> 576 us
+// per frame at 8 in flight (+30 %; thresholds 16 / 48: +24 % / +36 %), pass A 20.8 -> 17.7 lanes
+// active with 32 % more VALU and 50 % more vector-memory instructions per wave (the walk's
+// per-step bookkeeping, and the wave-uniform node fetch rarely fires once lanes are out of
+// step).  Kept as an opt-in experiment.
+#ifndef TRT_DEFER_REFILL
+#define TRT_DEFER_REFILL 0
+#endif
+#ifndef TRT_REFILL_T
+#define TRT_REFILL_T 32
+#endif
+template <int GEOM>
+constexpr bool defer_refill() {
+    return GEOM == 3 && TRT_DEFER_REFILL && !TRT_BVH_COMPRESS && TRT_BVH_QUANT && TRT_BVH_WIDTH == 4;
+}
+__device__ __forceinline__ bool defer_use_q(const KArgs& A) { return A.bvh4 && A.bvh4q && A.nbatch != 0; }
+template <bool SPLIT>
+__device__ __forceinline__ void defer_walk_q(const KArgs& A, float* lds, float4* slab, EvLog& L, bool have, Seg cur,
+                                             uint32_t link, uint32_t pix) {
+    lds_f32* P = (lds_f32*)lds;
+    Cnt cnt;
+    PSeg priv[kMaxTreeDepth];
+    int pn = 0;
+    uint32_t pool_n = 0; // wave-uniform
+    using Stack = BvhStack<bvh_lds_entries<3>(), false>;
+    typename Stack::Mem stack_mem;
+    Stack stack(slab, stack_mem);
+    enum : int { IDLE = 0, START = 1, TRAV = 2, DONE = 3 };
+    int ph = have ? START : IDLE;
+    Hit h;
+    h.kind = HIT_NONE;
+    f3 inv = mk(0.0f, 0.0f, 0.0f);
+    uint32_t node = 0;
+    float best = 0.0f;
+    for (;;) {
+        bool got;
+        pool_refill(P, pool_n, priv, pn, ph == IDLE, got, cur, link, pix);
+        if (got) ph = START;
+        if (__ballot(ph != IDLE) == 0ull) break;
+        if (ph == START) { // floor and spheres (scene_intersect), then the walk from the root
+            h.t = 1e10f;
+            h.kind = HIT_NONE;
+            h.idx = 0;
+            h.u = 0.0f;
+            h.v = 0.0f;
+            h.ni = 0;
+            h.batch = 0;
+            const f3 o = cur.o, d = cur.d;
+            if (A.flags & TRT_FLAG_FLOOR) { // shader.comp:302-320
+                if (fabsf(d.y) > TRT_EPS) {
+                    float t = div_rn(-(o.y + 4.0f), d.y);
+                    if (t > TRT_EPS && t < h.t) {
+                        f3 p = add(o, muls(d, t));
+                        if (fabsf(p.x) < 10.0f && p.z < -5.0f && p.z > -30.0f) {
+                            h.t = t;
+                            h.kind = HIT_FLOOR;
                         }
                     }
                 }
             }
-        }
-        const uint64_t pm = __ballot(have_other);
-        if (pm != 0ull) {
-            const uint32_t room = kPool - pool_n;
-            wave_lds_sync(); // this step's takes have read the entries the pushes may reuse
-            if (have_other) {
-                const uint32_t r = lane_rank(pm);
-                if (r < room) pool_put(P, pool_n + r, other);
-                else priv[pn++] = other;
+            if (A.flags & TRT_FLAG_SPHERES) { // shader.comp:322-335
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float t = 1e10f;
+                    if (sphere_hit(o, d, A.sph[i], t) && t < h.t) {
+                        h.t = t;
+                        h.kind = HIT_SPHERE;
+                        h.idx = i;
+                    }
+                }
             }
-            pool_n += min((uint32_t)__popcll(pm), room);
-            wave_lds_sync(); // the pushes land before the next step's takes
+            if (A.nbatch == 0 || ray_misses_all_batches(o, d)) {
+                ph = DONE;
+            } else {
+                inv = cull_inv(d);
+                node = 0u;
+                best = h.t;
+                stack.sp = 0;
+                ph = TRAV;
+            }
+        }
+        for (;;) { // walk steps
+            const uint64_t tm = __ballot(ph == TRAV);
+            if (tm == 0ull) break;
+            if ((uint32_t)__popcll(tm) < (uint32_t)TRT_REFILL_T && __ballot(ph == DONE) != 0ull) break;
+            if (ph == TRAV) {
+                bool more = false;
+                if (!(node & kBvhLeafBit)) {
+                    float4 pe;
+                    uint4 qa, qb, ch;
+                    const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
+                    if (__ballot(node != n0) == 0ull) { // every walking lane on one node: scalar loads
+                        typedef __attribute__((address_space(4))) const float cfloat;
+                        typedef __attribute__((address_space(4))) const uint32_t cuint;
+                        const cfloat* R = (const cfloat*)(A.bvh4q + n0);
+                        const cuint* RC = (const cuint*)(A.bvh4q + n0);
+                        pe = make_float4(R[0], R[1], R[2], R[3]);
+                        qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
+                        qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
+                        ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
+                    } else {
+                        const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
+                        pe = p[0];
+                        qa = reinterpret_cast<const uint4*>(p)[1];
+                        qb = reinterpret_cast<const uint4*>(p)[2];
+                        ch = reinterpret_cast<const uint4*>(p)[3];
+                    }
+                    more = visit4q<false>(cur.o, inv, best, pe, qa, qb, ch, stack, node, cnt);
+                } else {
+                    bvh_leaf<false, false>(A, node, cur.o, cur.d, inv, h, 0.0f, best, cnt);
+                }
+                if (!more) {
+                    if (stack.sp == 0) ph = DONE;
+                    else node = stack.pop();
+                }
+            }
+        }
+        const uint64_t dm = __ballot(ph == DONE);
+        if (dm != 0ull) { // shade the finished lanes together (one event row)
+            const uint32_t slot = ev_alloc(A, L);
+            bool have_other = false;
+            PSeg other;
+            if (ph == DONE) {
+                bool cont;
+                defer_shade<SPLIT>(A, L, slot, h, cur, link, pix, cont, other, have_other);
+                ph = cont ? START : IDLE;
+            }
+            pool_offer(P, pool_n, priv, pn, have_other, other);
         }
     }
 }
@@ -2163,6 +2330,12 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
         static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
         const size_t o = valid ? (size_t)k * A.width + x : 0u;
         const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
+        if constexpr (defer_refill<GEOM>()) {
+            if (defer_use_q(A)) {
+                defer_walk_q<SPLIT>(A, lds, slab, L, valid, root, kEvRoot, (uint32_t)o);
+                return;
+            }
+        }
         defer_walk<GEOM, SPLIT>(A, lds, slab, L, valid, root, kEvRoot, (uint32_t)o);
         return;
     }
@@ -2462,6 +2635,12 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
             EvLog L;
             // wave-uniform (ev_alloc and the query appends reserve from one stripe per wave)
             L.stripe = ((base / 64u + 0x5bd1e995u * A.split_d1) * 0x9E3779B1u) >> (32 - 7);
+            if constexpr (defer_refill<GEOM>()) {
+                if (defer_use_q(A)) {
+                    defer_walk_q<true>(A, lds, slab, L, valid, root, link, pixel);
+                    continue;
+                }
+            }
             defer_walk<GEOM, true>(A, lds, slab, L, valid, root, link, pixel);
             continue;
         }
@@ -2524,9 +2703,97 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
 // lanes sit at a hit.  Static schedule: wave w takes stripe w % kDeferStripes and every
 // (gridDim / kDeferStripes)-th 64-query block of it.  An occluded query ORs its light's bit
 // into its event.
+// Pass B with the any-hit walk turned inside out (GEOM 3, as defer_walk_q): each lane takes the
+// wave's next query as soon as its walk ends (early exits on an occluder make the walks' lengths
+// differ a lot), one node visit or leaf test per step.  The answer is shadow_intersect's: any
+// accepted occluder, in any order.  Measured and rejected (round 4): the shipped frame +5 % over
+// the per-query pass B (profiles/r04d_ab_deep.jsonl); opt-in (TRT_SHADOW_REFILL).
+#ifndef TRT_SHADOW_REFILL
+#define TRT_SHADOW_REFILL 0
+#endif
+__device__ __forceinline__ void defer_shadows_q(const KArgs& A, float4* slab) {
+    const uint32_t s = blockIdx.x % kDeferStripes, K = gridDim.x / kDeferStripes, b0 = blockIdx.x / kDeferStripes;
+    const uint32_t n = min(A.dctr->nq[s * kCtrStride], A.shq_cap);
+    const float4* Q = A.shq + 2 * (size_t)s * A.shq_cap;
+    // this wave's queries: its 64-query blocks b0, b0 + K, ... in order, ticket by ticket
+    auto qidx = [&](uint32_t t) { return (b0 + (t >> 6) * K) * 64u + (t & 63u); };
+    using Stack = BvhStack<bvh_lds_entries<3>(), false>;
+    typename Stack::Mem stack_mem;
+    Stack stack(slab, stack_mem);
+    Cnt cnt;
+    Hit unused;
+    bool walking = false;
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = o, inv = o;
+    float maxd = 0.0f, best = 0.0f;
+    uint32_t node = 0, tag = 0, tick = 0; // tick: wave-uniform
+    for (;;) {
+        const uint64_t idle = __ballot(!walking);
+        const bool more = qidx(tick) < n;
+        if (idle != 0ull && more) {
+            const uint32_t i = qidx(tick + lane_rank(idle));
+            if (!walking && i < n) {
+                const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
+                o = mk(a.x, a.y, a.z);
+                d = mk(b.x, b.y, b.z);
+                maxd = a.w;
+                tag = __float_as_uint(b.w);
+                bool occ = false;
+                if (A.flags & TRT_FLAG_SPHERES) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float t = 1e10f;
+                        if (!occ && sphere_hit(o, d, A.sph[k], t) && t < maxd) occ = true;
+                    }
+                }
+                if (occ) {
+                    atomicOr(reinterpret_cast<uint32_t*>(ev_plane(A, tag >> 2, 3)) + 1, 1u << (tag & 3u));
+                } else if (!ray_misses_all_batches(o, d)) {
+                    inv = cull_inv(d);
+                    best = maxd;
+                    node = 0u;
+                    stack.sp = 0;
+                    walking = true;
+                }
+            }
+            tick += (uint32_t)__popcll(idle);
+        }
+        for (;;) { // walk steps
+            const uint64_t wm = __ballot(walking);
+            if (wm == 0ull) break;
+            if ((uint32_t)__popcll(wm) < (uint32_t)TRT_REFILL_T && qidx(tick) < n) break;
+            if (walking) {
+                bool next = false, occ = false;
+                if (!(node & kBvhLeafBit)) {
+                    const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
+                    const float4 pe = p[0];
+                    const uint4 qa = reinterpret_cast<const uint4*>(p)[1], qb = reinterpret_cast<const uint4*>(p)[2],
+                                ch = reinterpret_cast<const uint4*>(p)[3];
+                    next = visit4q<false>(o, inv, best, pe, qa, qb, ch, stack, node, cnt);
+                } else {
+                    occ = bvh_leaf<false, true>(A, node, o, d, inv, unused, maxd, best, cnt);
+                }
+                if (occ) {
+                    atomicOr(reinterpret_cast<uint32_t*>(ev_plane(A, tag >> 2, 3)) + 1, 1u << (tag & 3u));
+                    walking = false;
+                } else if (!next) {
+                    if (stack.sp == 0) walking = false;
+                    else node = stack.pop();
+                }
+            }
+        }
+        if (__ballot(walking) == 0ull && !(qidx(tick) < n)) break;
+    }
+}
+
 template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    if constexpr (GEOM == 3 && TRT_SHADOW_REFILL && !TRT_BVH_COMPRESS && TRT_BVH_QUANT && TRT_BVH_WIDTH == 4) {
+        if (A.bvh4 && A.bvh4q && A.nbatch != 0) {
+            defer_shadows_q(A, slab);
+            return;
+        }
+    }
     Cnt cnt;
     const uint32_t s = blockIdx.x % kDeferStripes, K = gridDim.x / kDeferStripes;
     const uint32_t n = min(A.dctr->nq[s * kCtrStride], A.shq_cap);
