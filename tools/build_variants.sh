@@ -96,6 +96,9 @@ for v in "$@"; do
         t48) variant t48 -DTRT_REFILL_T=48 ;;
         t56) variant t56 -DTRT_REFILL_T=56 ;;
         srefill) variant srefill -DTRT_SHADOW_REFILL=1 ;;
+        dw5) variant dw5 -DTRT_DEFER_WAVES=5 ;;
+        dw6) variant dw6 -DTRT_DEFER_WAVES=6 ;;
+        dw5p96) variant dw5p96 -DTRT_DEFER_WAVES=5 -DTRT_DEFER_POOL=96 ;;
         pool192) variant pool192 -DTRT_DEFER_POOL=192 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac

@@ -2494,8 +2494,18 @@ constexpr int waves_per_simd() {
     return GEOM == 3 ? (CAP <= 3 ? TRT_G3_WAVES_SHALLOW : TRT_G3_WAVES) : GEOM == 0 ? TRT_G0_WAVES : TRT_WAVES;
 }
 
+// Waves per SIMD of pass A of a deferred frame (the quantized walk without shadow rays): 4 like
+// the other deep walks, or TRT_DEFER_WAVES.
+#ifndef TRT_DEFER_WAVES
+#define TRT_DEFER_WAVES 4
+#endif
+template <int GEOM, int CAP, bool SPLIT, bool DEFER>
+constexpr int trace_waves() {
+    return (DEFER && GEOM == 3) ? TRT_DEFER_WAVES : waves_per_simd<GEOM, ((SPLIT || DEFER) ? 99 : CAP)>();
+}
+
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
-__global__ __launch_bounds__(64 * TRT_WPB, (waves_per_simd<GEOM, ((SPLIT || DEFER) ? 99 : CAP)>())) void trace_kernel(KArgs A) {
+__global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void trace_kernel(KArgs A) {
 #if TRT_WPB > 1
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
     // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
