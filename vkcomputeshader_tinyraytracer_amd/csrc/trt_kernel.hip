@@ -57,6 +57,10 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
 #ifndef TRT_SKIP_DARK
 #define TRT_SKIP_DARK 1
 #endif
+// The specular term is not formed when its albedo weight is zero (cast_seg).
+#ifndef TRT_SPEC_SKIP
+#define TRT_SPEC_SKIP 1
+#endif
 #define TRT_PI 3.14159265358979323846f /* PI, shader.comp:82 */
 #define TRT_GAMMA 2.2f /* GAMMA, shader.comp:81 */
 
@@ -1627,12 +1631,15 @@ __device__ __forceinline__ LightTerm light_term(const KArgs& A, const Surf& s, f
     t.dist = length3(sub(L, s.p));
     t.so = dot3(t.ld, s.n) < 0.0f ? sub(s.p, muls(s.n, TRT_EPS)) : add(s.p, muls(s.n, TRT_EPS));
     t.diff = 1.0f * fmaxf(0.0f, dot3(s.n, t.ld));
-    const f3 rdir = reflect3(neg(t.ld), s.n);
+    t.spec = 0.0f; // not formed under a zero specular weight (cast_seg)
+    if (!TRT_SPEC_SKIP || s.alb[1] != 0.0f) {
+        const f3 rdir = reflect3(neg(t.ld), s.n);
 #ifdef TRT_DIAG_NO_POW
-    t.spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * s.sexp; // diagnostic: prices powf
+        t.spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * s.sexp; // diagnostic: prices powf
 #else
-    t.spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), s.sexp);
+        t.spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), s.sexp);
 #endif
+    }
     t.matters = TRT_SKIP_DARK == 0 || (s.alb[0] != 0.0f && t.diff != 0.0f) || (s.alb[1] != 0.0f && t.spec != 0.0f);
     return t;
 }
@@ -1765,12 +1772,17 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 float dist = length3(sub(L, p));
                 f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
                 const float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
-                const f3 rdir = reflect3(neg(ld), n);
+                // With a zero specular weight (the floor, the diffuse meshes) the specular sum only
+                // ever enters the colour as specular * 0 = 0 (it is finite), so it is not formed.
+                float spec = 0.0f;
+                if (!TRT_SPEC_SKIP || alb[1] != 0.0f) {
+                    const f3 rdir = reflect3(neg(ld), n);
 #ifdef TRT_DIAG_NO_POW
-                const float spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
+                    spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
 #else
-                const float spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
+                    spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
 #endif
+                }
                 // A light whose diffuse term and specular term both vanish from the colour (a
                 // zero term, or a zero albedo weight: diffuse * 0 = 0 for any finite diffuse)
                 // adds exactly nothing whether it is lit or shadowed, so its shadow query cannot
