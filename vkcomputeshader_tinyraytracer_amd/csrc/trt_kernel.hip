@@ -2527,7 +2527,11 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
     float* lds = lds_all + w * (DEFER ? defer_pool_floats() : lds_stack_floats<CAP>());
     float4* slab = slab_all + w * slab_float4s<GEOM>();
     const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
-    if (vb >= A.ntiles) return;
+    // virtual blocks of the launch: ntiles per frame, or per frame pair (multi-frame launches)
+    const uint32_t nvb = A.ntiles * ((!SPLIT && !DEFER && A.nframes > 1u)
+                                         ? (A.xcd_inter && A.frame_group > 1u ? (A.nframes + 1u) / 2u : A.nframes)
+                                         : 1u);
+    if (vb >= nvb) return;
 #else
     __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()];
     // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
@@ -3062,10 +3066,14 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
         return hipGetLastError();
     }
     // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)
-#if !defined(TRT_PERSIST) && !defined(TRT_TPW) && TRT_WPB == 1
+#if !defined(TRT_PERSIST) && !defined(TRT_TPW)
     const uint32_t fblocks = A.nframes > 1u && A.xcd_inter && A.frame_group > 1u ? (A.nframes + 1u) / 2u
                                                                                   : std::max(A.nframes, 1u);
+#if TRT_WPB == 1
     const dim3 fgrid(A.ntiles * fblocks);
+#else // TRT_WPB waves per workgroup: virtual blocks as in trace_kernel, whole groups of 8 blocks
+    const dim3 fgrid(((A.ntiles * fblocks + 8 * TRT_WPB - 1) / (8 * TRT_WPB)) * 8);
+#endif
 #else
     const dim3 fgrid = grid;
 #endif
