@@ -6,7 +6,11 @@
 Every frame has its own UBO: the camera walks like the reference's interactive loop with W and
 D held (processInput + updateUniformBuffer, main.cpp:391-403, 2165-2179), cycling through
 --camera-period positions whose ray counts come from one counting pass each (excluded from
-timing).  Inputs are resident in HBM; the timed region only enqueues and runs frames.
+timing).  Inputs are resident in HBM; the timed region only enqueues and runs frames.  Before
+it, untimed frames of the same loop run for --settle-ms (default 50): the MI355X raises its
+clocks over the first ~30 ms of sustained load, and a 20-step region (0.3 ms) timed from an idle
+GPU measured the ramp (C2 13.7 us per frame of kernel time cold, 12.2 settled,
+profiles/r04l_settle.jsonl).  The timed region itself holds exactly K full steps.
 
 * N = 1: one step = one frame.  The value is the native frame loop (trt_render_frames: plain
   frames go out as multi-frame launches) — `path` in the line says which path produced it; the
@@ -75,6 +79,9 @@ def parse():
     ap.add_argument("--traffic", default="live", choices=["live", "table", "off"],
                     help="roofline.traffic: live = two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over a "
                          "child run of the same frame loop (N = 1); table = the committed measurement")
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="untimed frames of the timed loop's own shape for this long before the timed "
+                         "region (clocks at their steady state)")
     ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N > 1 process shape (torch.distributed nccl group + trt_multi rank "
@@ -284,6 +291,16 @@ def timed(g: Group, fn) -> float:
     return g.max(time.perf_counter() - t0)
 
 
+def settle(args, fn) -> None:
+    """Runs fn (one untimed pass of the timed loop's first chunk) until args.settle_ms have passed."""
+    import torch
+
+    t_end = time.perf_counter() + max(0.0, getattr(args, "settle_ms", 0.0)) / 1e3
+    while time.perf_counter() < t_end:
+        fn()
+        torch.cuda.synchronize()
+
+
 def walk(scene, period: int):
     from vkcomputeshader_tinyraytracer_amd import camera_path
 
@@ -332,6 +349,7 @@ def frame_loop(dev: int, scene, frames: int, warmup: int, args, g: Group | None 
         r.render_frames(p, out8, max(1, min(warmup, ring)), ubos=ubos, frame_stride=fb)
         chunks = [(i0, min(ring, frames - i0)) for i0 in range(0, frames, ring)]
         ubo_chunks = [np.ascontiguousarray(ubos[i0:i0 + n]) for i0, n in chunks]
+        settle(args, lambda: r.render_frames(p, out8, chunks[0][1], ubos=ubo_chunks[0], frame_stride=fb))
 
         def run():
             for (_, n), u in zip(chunks, ubo_chunks):
@@ -399,11 +417,21 @@ def tiled_loop(g: Group, dev: int, multi, scene, frames: int, warmup: int, args,
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
     # warmup: one exchange of the timed size, so the timed batches never allocate
-    multi.render_frames(p, max(min(warmup, ring), min(per_gather, ring)), args.band_rows, root, per_gather,
-                        outs=[out], frame_stride=fb, ubos=ubos)
+    t0 = time.perf_counter()
+    warm_n = max(min(warmup, ring), min(per_gather, ring))
+    multi.render_frames(p, warm_n, args.band_rows, root, per_gather, outs=[out], frame_stride=fb, ubos=ubos)
+    torch.cuda.synchronize()
+    t_warm = g.max(time.perf_counter() - t0)
 
     chunks = [(i0, min(ring, frames - i0)) for i0 in range(0, frames, ring)]
     ubo_chunks = [np.ascontiguousarray(ubos[i0:i0 + n]) for i0, n in chunks]
+    # settle: the same number of untimed passes on every rank (they exchange), sized from the
+    # slowest rank's warmup time
+    t_chunk = max(t_warm * chunks[0][1] / warm_n, 1e-4)
+    for _ in range(int(np.ceil(args.settle_ms / 1e3 / t_chunk)) if args.settle_ms > 0 else 0):
+        multi.render_frames(p, chunks[0][1], args.band_rows, root, per_gather, outs=[out], frame_stride=fb,
+                            ubos=ubo_chunks[0])
+    torch.cuda.synchronize()
 
     def run():
         for (_, n), u in zip(chunks, ubo_chunks):
@@ -487,7 +515,13 @@ def tiled_frame(g: Group, dev: int, multi, frames: int, args) -> dict | None:
     torch.cuda.synchronize()
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
+    t0 = time.perf_counter()
     multi.render_frames(p, 2, args.band_rows, 0, 1, outs=[out])
+    torch.cuda.synchronize()
+    t_frame = max(g.max(time.perf_counter() - t0) / 2, 1e-4)
+    if args.settle_ms > 0:  # the same untimed frame count on every rank (they exchange)
+        multi.render_frames(p, int(min(1000, -(-args.settle_ms / 1e3 // t_frame))), args.band_rows, 0, 1, outs=[out])
+        torch.cuda.synchronize()
     elapsed = timed(g, lambda: multi.render_frames(p, frames, args.band_rows, 0, 1, outs=[out]))
     multi.set_stream(0, None)
     rays = rays_of(st)
@@ -564,7 +598,7 @@ def _pmc_pass(counter: str, args, outdir: Path) -> list[dict]:
     cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", str(outdir),
            "-o", "run", "--", sys.executable, str(REPO / "bench.py"), "--traffic-probe", "--config", args.config,
            "--steps", str(probe_steps(args)), "--warmup", str(args.warmup), "--inflight", str(args.inflight),
-           "--frame-batch", str(args.frame_batch), "--camera-period", str(args.camera_period)]
+           "--frame-batch", str(args.frame_batch), "--camera-period", str(args.camera_period), "--settle-ms", "0"]
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     subprocess.run(cmd, check=True, timeout=240, env=env, cwd="/tmp", stdout=subprocess.DEVNULL,
                    stderr=subprocess.DEVNULL)
@@ -764,6 +798,7 @@ def main():
                 "parallelism": parallelism,
                 "frames_per_step": world,
                 "launches": fl["launches"],
+                "settle_ms": args.settle_ms,
                 "last_frame_matches_trt_render": plain_ok if not dist_mode else tiled_ok,
                 "value_form": "frame per GPU, plain loop" if not dist_mode else
                               "weak: N frames per step, each row-tiled over all ranks, rotating roots",

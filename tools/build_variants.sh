@@ -26,6 +26,7 @@ variant() { # name extra-flags...
 for v in "$@"; do
     case $v in
         base) variant base ;;
+        cur) variant cur ;;
         unode) variant unode -DTRT_UNIFORM_NODE=1 ;;
         g0w4) variant g0w4 -DTRT_G0_WAVES=1 ;;
         g3lds8) variant g3lds8 -DTRT_G3_LDS=8 ;;

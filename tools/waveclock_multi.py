@@ -42,13 +42,14 @@ def analyse(raw, F):
     above = np.nonzero(conc >= peak / 2)[0]
     tail_start = float(ev[above[-1] + 1, 0]) if len(above) and above[-1] + 1 < len(ev) else span
     dur = e - s
-    last = frame == F - 1
+    last = frame == frame.max()
     return {
         "frames": F, "workgroups": int(len(raw)), "span_us": span / 1e3, "peak_resident": peak,
         "ideal_us": float(dur.sum() / peak) / 1e3, "ramp_to_95pct_peak_us": ramp / 1e3,
         "tail_below_half_peak_us": (span - tail_start) / 1e3,
         "last_start_us": float(s.max()) / 1e3,
-        "frame_end_us": [round(float(e[frame == f].max()) / 1e3, 2) for f in range(F)],
+        # frame pairs record their first frame only (the block traces frames 2p and 2p + 1)
+        "frame_end_us": [round(float(e[frame == f].max()) / 1e3, 2) for f in range(F) if (frame == f).any()],
         "dur_us_all": {q: round(float(np.percentile(dur, q)) / 1e3, 2) for q in (50, 90, 99, 100)},
         "dur_us_last_frame": {q: round(float(np.percentile(dur[last], q)) / 1e3, 2) for q in (50, 90, 99, 100)},
         "last_frame_longest_start_us": round(float(s[last][np.argmax(dur[last])]) / 1e3, 2),
