@@ -417,21 +417,26 @@ def tiled_loop(g: Group, dev: int, multi, scene, frames: int, warmup: int, args,
     stream = torch.cuda.Stream()
     multi.set_stream(0, stream)
     # warmup: one exchange of the timed size, so the timed batches never allocate
-    t0 = time.perf_counter()
-    warm_n = max(min(warmup, ring), min(per_gather, ring))
-    multi.render_frames(p, warm_n, args.band_rows, root, per_gather, outs=[out], frame_stride=fb, ubos=ubos)
-    torch.cuda.synchronize()
-    t_warm = g.max(time.perf_counter() - t0)
+    multi.render_frames(p, max(min(warmup, ring), min(per_gather, ring)), args.band_rows, root, per_gather,
+                        outs=[out], frame_stride=fb, ubos=ubos)
 
     chunks = [(i0, min(ring, frames - i0)) for i0 in range(0, frames, ring)]
     ubo_chunks = [np.ascontiguousarray(ubos[i0:i0 + n]) for i0, n in chunks]
-    # settle: the same number of untimed passes on every rank (they exchange), sized from the
-    # slowest rank's warmup time
-    t_chunk = max(t_warm * chunks[0][1] / warm_n, 1e-4)
-    for _ in range(int(np.ceil(args.settle_ms / 1e3 / t_chunk)) if args.settle_ms > 0 else 0):
+
+    def chunk0():
         multi.render_frames(p, chunks[0][1], args.band_rows, root, per_gather, outs=[out], frame_stride=fb,
                             ubos=ubo_chunks[0])
-    torch.cuda.synchronize()
+
+    # settle: the same number of untimed passes on every rank (they exchange), sized from the
+    # slowest rank's time for one pass (after the allocating warmup above)
+    if args.settle_ms > 0:
+        t0 = time.perf_counter()
+        chunk0()
+        torch.cuda.synchronize()
+        t_chunk = max(g.max(time.perf_counter() - t0), 1e-4)
+        for _ in range(int(np.ceil(args.settle_ms / 1e3 / t_chunk))):
+            chunk0()
+        torch.cuda.synchronize()
 
     def run():
         for (_, n), u in zip(chunks, ubo_chunks):

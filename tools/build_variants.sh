@@ -27,6 +27,8 @@ for v in "$@"; do
     case $v in
         base) variant base ;;
         cur) variant cur ;;
+        g3p24) variant g3p24 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=24 ;;
+        g3p32) variant g3p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 ;;
         unode) variant unode -DTRT_UNIFORM_NODE=1 ;;
         g0w4) variant g0w4 -DTRT_G0_WAVES=1 ;;
         g3lds8) variant g3lds8 -DTRT_G3_LDS=8 ;;

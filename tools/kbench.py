@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--defer", type=int, default=0, help="deferred shadows (0 auto, 1 off, 2 on)")
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=None, help="override trt_params.flags")
     ap.add_argument("--frame-batch", type=int, default=0, help="frames per launch (0 auto, 1 = one per frame)")
+    ap.add_argument("--settle-ms", type=float, default=50.0, help="untimed frames first for this long (clock ramp)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -62,6 +63,11 @@ def main():
     r.set_deferred_shadows(a.defer)
     r.set_frame_batch(a.frame_batch)
     r.render_frames(p, out, 5)
+    import time
+    t_end = time.perf_counter() + a.settle_ms / 1e3
+    while time.perf_counter() < t_end:
+        r.render_frames(p, out, a.frames)
+        torch.cuda.synchronize()
     nt = r.render_frames(p, out, a.frames, timing=True)
     ms = r.frame_times(nt)  # per frame of each launch
     torch.cuda.synchronize()

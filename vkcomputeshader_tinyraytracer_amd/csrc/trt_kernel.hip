@@ -756,6 +756,14 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 #ifndef TRT_SHADOW_SHARE
 #define TRT_SHADOW_SHARE 0
 #endif
+// GEOM 3 kernels walk the quantized nodes only (the host picks GEOM 3 only when they exist):
+// the 64-B-node and binary walks are not compiled into them, so the register allocation of
+// the 96-VGPR (5-wave) build sees one walk per call site.
+#ifndef TRT_G3_QONLY
+#define TRT_G3_QONLY 1
+#endif
+template <int GEOM>
+constexpr bool g3_quant_only() { return GEOM == 3 && TRT_G3_QONLY && TRT_BVH_QUANT && !TRT_BVH_COMPRESS; }
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
@@ -822,7 +830,7 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 #if TRT_BVH_QUANT
     // measured: -3 % on C4 (1,600 batches, 4-wave build), +2..3 % on C3 / the shipped frame
     // (profiles/r02_ab_quant.log), so the quantized nodes serve the 4-wave build only
-    if (GEOM == 3 && A.bvh4q) {
+    if (GEOM == 3 && (g3_quant_only<GEOM>() || A.bvh4q)) {
         {
             typedef __attribute__((address_space(4))) const float cfloat;
             typedef __attribute__((address_space(4))) const uint32_t cuint;
@@ -985,6 +993,7 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 #endif
     }
 #endif
+    if constexpr (g3_quant_only<GEOM>()) return;
 #if TRT_ROOT_SCALAR
     {
         // constant address space: the compiler may (and, the address being uniform, does) use
@@ -1199,7 +1208,7 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
     f3 inv = GEOM >= 2 ? cull_inv(d) : mk(rcp_rn_lane(d.x), rcp_rn_lane(d.y), rcp_rn_lane(d.z)); // shader.comp:336
     bool unused = false;
     if (GEOM >= 2) {
-        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
+        if (g3_quant_only<GEOM>() || (TRT_BVH_WIDTH == 4 && A.bvh4)) trace_bvh4<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
         else trace_bvh<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
     }
     else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
@@ -1253,7 +1262,7 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
                     return shadow_wave_q(A, o, d, inv, max_dist, slab);
             }
 #endif
-        if (TRT_BVH_WIDTH == 4 && A.bvh4) trace_bvh4<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
+        if (g3_quant_only<GEOM>() || (TRT_BVH_WIDTH == 4 && A.bvh4)) trace_bvh4<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
         else trace_bvh<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
     }
     else walk_batches<COUNT, true>(A, o, d, inv, unused, occluded, max_dist, c, slab);
@@ -1399,9 +1408,15 @@ struct Seg {
 // Split launches (trace in depth windows) use a hybrid: the window's entries in LDS and a
 // private tail that only a child traced in place after a full task queue can reach.
 constexpr int LDS_STACK_MAX = 4;
-
-template <int CAP>
-constexpr int lds_stack_floats() { return (CAP >= 1 && CAP <= LDS_STACK_MAX) ? CAP * 8 * 64 : 1; }
+// TRT_G3_SEG_PRIV: the per-pixel loop of GEOM 3 kernels (not split) keeps its deferred children
+// in a private array, and the LDS goes to the BVH traversal stack (TRT_G3_LDS entries).
+#ifndef TRT_G3_SEG_PRIV
+#define TRT_G3_SEG_PRIV 0
+#endif
+template <int CAP, int GEOM = 0, bool HYB = false>
+constexpr bool seg_lds() { return CAP >= 1 && CAP <= LDS_STACK_MAX && (HYB || !(GEOM == 3 && TRT_G3_SEG_PRIV)); }
+template <int CAP, int GEOM = 0, bool HYB = false>
+constexpr int lds_stack_floats() { return seg_lds<CAP, GEOM, HYB>() ? CAP * 8 * 64 : 1; }
 
 template <int CAP, bool LDS = (CAP <= LDS_STACK_MAX)>
 struct DeferStack;
@@ -1471,12 +1486,12 @@ struct HybridStack {
     }
 };
 
-template <int CAP, bool SPLIT>
+template <int CAP, bool SPLIT, int GEOM = 0>
 struct StackOf {
-    using type = DeferStack<CAP>;
+    using type = DeferStack<CAP, seg_lds<CAP, GEOM>()>;
 };
-template <int CAP>
-struct StackOf<CAP, true> {
+template <int CAP, int GEOM>
+struct StackOf<CAP, true, GEOM> {
     using type = HybridStack<CAP, (int)TRT_MAX_DEPTH_LIMIT - 1 - CAP>;
 };
 
@@ -1684,7 +1699,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                                        uint32_t pixel, bool& spilled) {
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    using Stk = typename StackOf<CAP, HYB>::type;
+    using Stk = typename StackOf<CAP, HYB, GEOM>::type;
     typename Stk::Mem stk_mem;
     Stk stk(lds, stk_mem);
     for (;;) {
@@ -2521,10 +2536,10 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
 #if TRT_WPB > 1
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
     // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
-    __shared__ float lds_all[(DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()) * TRT_WPB];
+    __shared__ float lds_all[(DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>()) * TRT_WPB];
     __shared__ float4 slab_all[slab_float4s<GEOM>() * TRT_WPB];
     const uint32_t w = threadIdx.x >> 6;
-    float* lds = lds_all + w * (DEFER ? defer_pool_floats() : lds_stack_floats<CAP>());
+    float* lds = lds_all + w * (DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>());
     float4* slab = slab_all + w * slab_float4s<GEOM>();
     const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
     // virtual blocks of the launch: ntiles per frame, or per frame pair (multi-frame launches)
@@ -2533,7 +2548,7 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
                                          : 1u);
     if (vb >= nvb) return;
 #else
-    __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()];
+    __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>()];
     // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
     __shared__ float4 slab[slab_float4s<GEOM>()];
     const uint32_t vb = blockIdx.x;
@@ -2638,7 +2653,7 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
 // segment pool (defer_walk).
 template <int CAP, bool COUNT, int GEOM, bool DEFER = false>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs A) {
-    __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP>()];
+    __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, true>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = min(*A.q_in_n, A.q_cap);
@@ -2900,7 +2915,7 @@ __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
 // by the per-pixel loop with in-place shadow rays (persistent waves over the list).
 template <int CAP, int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KArgs A) {
-    __shared__ float lds[lds_stack_floats<CAP>()];
+    __shared__ float lds[lds_stack_floats<CAP, GEOM, false>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = A.dctr->nfb;

@@ -632,7 +632,9 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // since the traversal stack's index left scratch memory (round 3) it is ahead or equal
     // everywhere: C4 2.90 vs 3.38 ms, C3 -9 %, shipped frame and README scene within 1 %
     // (profiles/r03_ab_waves4_after_stack_fix.log), so it is the default for every BVH scene.
-    A.bvh_waves4 = c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : 1u;
+    // GEOM 3 kernels walk only the quantized nodes (trt_kernel.hip g3_quant_only): a scene whose
+    // nodes did not quantize (or whose 4-wide stack would not fit) takes the GEOM 2 kernels.
+    A.bvh_waves4 = c->d_bvh4q ? (c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : 1u) : 0u;
     A.xcd_rot = c->xcd_rot;
     A.xcd_skew = c->xcd_skew;
     A.xcd_inter = c->xcd_inter;
