@@ -295,6 +295,38 @@ def test_frame_loop_matches_single_frames(gpu_renderer):
         assert np.array_equal(out[i].cpu().numpy(), one)
 
 
+def test_prepared_frame_list_matches_render_frames(gpu_renderer):
+    """Renderer.frames_call (the bench's timed loop: checks done once, one native call per
+    issue) renders what render_frames renders, and re-issuing it renders the same frames."""
+    torch = pytest.importorskip("torch")
+    sc = S.config_c2(96, 64, env_size=SMALL_ENV)
+    gpu_renderer.upload_scene(sc)
+    ubos = np.stack([S.make_ubo(cam=(0.1 * i, 0.0, -0.2 * i)) for i in range(5)])
+    fb = 64 * 96 * 4
+    a = torch.zeros((5, 64, 96, 4), dtype=torch.uint8, device="cuda")
+    b = torch.zeros_like(a)
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()
+    gpu_renderer.set_stream(stream)
+    try:
+        gpu_renderer.render_frames(sc.params(), a, 5, ubos=ubos, frame_stride=fb)
+        call = gpu_renderer.frames_call(sc.params(), b, 5, ubos=ubos, frame_stride=fb)
+        call()
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        b.zero_()
+        torch.cuda.synchronize()
+        call()
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        with pytest.raises(ValueError):
+            gpu_renderer.frames_call(sc.params(), b[:2], 5, ubos=ubos, frame_stride=fb)
+        with pytest.raises(ValueError):
+            gpu_renderer.frames_call(sc.params(), b, 5, ubos=ubos[:3], frame_stride=fb)
+    finally:
+        gpu_renderer.set_stream(None)
+
+
 def _moving_ubos(n, sphere_every=0):
     """Per-frame UBOs: the camera moves every frame (main.cpp:391-403); with sphere_every > 0
     sphere 0 also moves every sphere_every frames, which splits a multi-frame launch there."""

@@ -29,6 +29,10 @@ for v in "$@"; do
         cur) variant cur ;;
         g3p24) variant g3p24 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=24 ;;
         g3p32) variant g3p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 ;;
+        g3p16) variant g3p16 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=16 ;;
+        g3p20) variant g3p20 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=20 ;;
+        g3p28) variant g3p28 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=28 ;;
+        g3w4p32) variant g3w4p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 -DTRT_G3_WAVES_SHALLOW=4 ;;
         unode) variant unode -DTRT_UNIFORM_NODE=1 ;;
         g0w4) variant g0w4 -DTRT_G0_WAVES=1 ;;
         g3lds8) variant g3lds8 -DTRT_G3_LDS=8 ;;

@@ -350,11 +350,15 @@ __device__ __forceinline__ bool bvh_box(f3 o, f3 inv, const float* lo, const flo
 constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 
 // GEOM 3 is the BVH walk compiled for 4 waves per SIMD (<= 128 VGPRs), or 5 (<= 96 VGPRs)
-// for plain frames of max_depth <= 4 (CAP <= 3, TRT_G3_WAVES_SHALLOW), with an 8-entry LDS
-// stack: 20 waves of (2 KB stack + 6 KB deferred segments) fill a CU's 160 KB.  8 and 16
-// entries tie at 4 waves (profiles/r03_ab_g3_lds_stack.log); 5 waves: C4 2.69 -> 2.63 ms,
-// depth-2 C4 -5.5 %, C3 within noise (profiles/r03_ab_g5.log).  CAP 4 (max_depth 5) needs
-// 8 KB of deferred segments and does not reach 5 waves, so deeper frames stay at 4.
+// for plain frames of max_depth <= 4 (CAP <= 3, TRT_G3_WAVES_SHALLOW): 5 waves: C4 2.69 ->
+// 2.63 ms, depth-2 C4 -5.5 %, C3 within noise (profiles/r03_ab_g5.log).  LDS per wave: the
+// traversal stack's first TRT_G3_LDS entries (16: 4 KB).  Round 3 kept 8 entries beside 6 KB
+// of deferred children (20 waves x 8 KB fill a CU's 160 KB); the children now live in a
+// private array (TRT_G3_SEG_PRIV: a glass hit's rare push) and the stack takes the LDS:
+// C4 2.626 -> 2.505 ms, C3 -5.7 %, the deferred frames unchanged; 16, 20, 24, 28 entries tie,
+// 32 entries and the 4-wave build with them are slower (profiles/r04o_ab_g3_lds_stack.jsonl,
+// r04p_ab_g3_lds_sweep.jsonl).  16 leaves pass A of deferred frames (5 KB segment pool + the
+// stack) at 4 waves per SIMD.
 #ifndef TRT_G3_WAVES
 #define TRT_G3_WAVES 4
 #endif
@@ -362,7 +366,7 @@ constexpr int kBvhLdsStack = TRT_BVH_LDS ? TRT_BVH_LDS_N : 0;
 #define TRT_G3_WAVES_SHALLOW 5
 #endif
 #ifndef TRT_G3_LDS
-#define TRT_G3_LDS 8
+#define TRT_G3_LDS 16
 #endif
 template <int GEOM>
 constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS : 0) : kBvhLdsStack; }
@@ -1409,9 +1413,10 @@ struct Seg {
 // private tail that only a child traced in place after a full task queue can reach.
 constexpr int LDS_STACK_MAX = 4;
 // TRT_G3_SEG_PRIV: the per-pixel loop of GEOM 3 kernels (not split) keeps its deferred children
-// in a private array, and the LDS goes to the BVH traversal stack (TRT_G3_LDS entries).
+// in a private array, and the LDS goes to the BVH traversal stack (TRT_G3_LDS entries): a
+// child is pushed once per glass hit, a traversal entry several times per ray.
 #ifndef TRT_G3_SEG_PRIV
-#define TRT_G3_SEG_PRIV 0
+#define TRT_G3_SEG_PRIV 1
 #endif
 template <int CAP, int GEOM = 0, bool HYB = false>
 constexpr bool seg_lds() { return CAP >= 1 && CAP <= LDS_STACK_MAX && (HYB || !(GEOM == 3 && TRT_G3_SEG_PRIV)); }

@@ -175,6 +175,36 @@ class Renderer:
                                               nframes, out8.data_ptr(), frame_stride, time_every))
         return int(self._L.trt_timed_launches(self._h, None, 0)) if timing else 0
 
+    def frames_call(self, params: T.Params, out8, nframes: int, ubos: np.ndarray | None = None,
+                    frame_stride: int = 0):
+        """render_frames(params, out8, nframes, ubos, frame_stride) with its argument checks and
+        conversions done once: returns a zero-argument callable that only enqueues the frames
+        (one trt_render_frames call), for host loops that re-issue the same frame list."""
+        if not _is_torch_cuda(out8):
+            raise ValueError("render_frames renders into a device (torch CUDA) tensor")
+        p = T.Params.from_buffer_copy(params)
+        p.flags |= T.FLAG_DEVICE_PTRS
+        p.flags &= ~(T.FLAG_COUNT | T.FLAG_TIMING)
+        rows = p.height if p.flags & T.FLAG_BAND_IN_PLACE else int(self._L.trt_output_rows(ctypes.byref(p)))
+        need = rows * p.width * 4 + max(nframes - 1, 0) * frame_stride
+        if not out8.is_contiguous() or out8.dtype.itemsize != 1 or out8.numel() < need:
+            raise ValueError(f"out8 must be a contiguous uint8 tensor of >= {need} bytes")
+        u = None
+        if ubos is not None:
+            u = np.ascontiguousarray(ubos, T.UBO)
+            if u.shape[0] < nframes:
+                raise ValueError(f"{u.shape[0]} UBOs for {nframes} frames")
+        fn, h, pp = self._L.trt_render_frames, self._h, ctypes.byref(p)
+        up, op = (u.ctypes.data if u is not None else None), out8.data_ptr()
+        keep = (p, u, out8)  # alive as long as the callable
+
+        def call() -> None:
+            rc = fn(h, pp, up, nframes, op, frame_stride, 0)
+            if rc:
+                self._check(rc)
+        call.keep = keep
+        return call
+
     def frame_times(self, n: int) -> np.ndarray:
         """Device ms per frame of each of the first n timed launches (span / frames traced)."""
         ms = (ctypes.c_float * n)()
