@@ -1421,7 +1421,27 @@ constexpr int LDS_STACK_MAX = 4;
 template <int CAP, int GEOM = 0, bool HYB = false>
 constexpr bool seg_lds() { return CAP >= 1 && CAP <= LDS_STACK_MAX && (HYB || !(GEOM == 3 && TRT_G3_SEG_PRIV)); }
 template <int CAP, int GEOM = 0, bool HYB = false>
-constexpr int lds_stack_floats() { return seg_lds<CAP, GEOM, HYB>() ? CAP * 8 * 64 : 1; }
+constexpr int lds_stack_floats_() { return seg_lds<CAP, GEOM, HYB>() ? CAP * 8 * 64 : 1; }
+// TRT_G3_PARK: with the deferred children out of LDS, the GEOM 3 per-pixel loop parks the
+// shading state its shadow walks do not use (colour, throughput, depth, the child weights and
+// index of refraction, the ray direction, kd, the exponent, the diffuse weight: 16 floats per
+// lane, 4 KB per wave) in LDS around the walks, instead of the register allocator spilling it to
+// scratch (the 96-VGPR 5-wave build).  Measured: the static spill reloads fall (232 -> 164) but
+// C4 +6.4 %, C3 +6.3 %, the README scene +3.6 % (profiles/r04s_ab_g3_park_rejected.jsonl: the
+// compiler-level fences and LDS round trips cost more than the scratch they replace), so off.
+#ifndef TRT_G3_PARK
+#define TRT_G3_PARK 0
+#endif
+constexpr int kParkFields = 16;
+template <int GEOM, bool HYB>
+constexpr bool park_state() { return GEOM == 3 && TRT_G3_PARK && TRT_G3_SEG_PRIV && !HYB; }
+template <int CAP, int GEOM = 0, bool HYB = false>
+constexpr int lds_stack_floats() {
+    return park_state<GEOM, HYB>() ? kParkFields * 64 : lds_stack_floats_<CAP, GEOM, HYB>();
+}
+// A compiler-only memory barrier: parked values are read back from LDS, not forwarded from the
+// registers that stored them (which would keep them live across the walks).
+__device__ __forceinline__ void park_fence() { asm volatile("" ::: "memory"); }
 
 template <int CAP, bool LDS = (CAP <= LDS_STACK_MAX)>
 struct DeferStack;
@@ -1785,8 +1805,32 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             f3 v = neg(cur.d);
             f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
             f3 kdv = mk(kd[0], kd[1], kd[2]);
+            // PARK (GEOM 3): what the light loop does not need during its shadow walks waits in
+            // this lane's LDS column (park_state) and is read back after each walk / the loop.
+            constexpr bool PARK = park_state<GEOM, HYB>();
+            lds_f32* const P = (lds_f32*)(lds + lane_id());
+            if constexpr (PARK) {
+                const float f[kParkFields] = {color.x, color.y, color.z, cur.thr, __int_as_float(cur.depth), alb[2],
+                                              alb[3], ior, cur.d.x, cur.d.y, cur.d.z, kd[0], kd[1], kd[2], sexp, alb[0]};
+#pragma unroll
+                for (int k = 0; k < kParkFields; ++k) P[k * 64] = f[k];
+            }
+            auto park_v = [&]() -> f3 {
+                if constexpr (PARK) return neg(mk(P[8 * 64], P[9 * 64], P[10 * 64]));
+                else return v;
+            };
+            auto park_kd = [&]() -> f3 {
+                if constexpr (PARK) return mk(P[11 * 64], P[12 * 64], P[13 * 64]);
+                else return kdv;
+            };
+            auto park_f = [&](int k, float x) -> float {
+                if constexpr (PARK) return P[k * 64];
+                else return x;
+            };
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
+                if constexpr (PARK) park_fence();
+                const float sexp_i = park_f(14, sexp), alb0_i = park_f(15, alb[0]);
                 f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
                 f3 ld = normalize3(sub(L, p));
                 float dist = length3(sub(L, p));
@@ -1798,9 +1842,9 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 if (!TRT_SPEC_SKIP || alb[1] != 0.0f) {
                     const f3 rdir = reflect3(neg(ld), n);
 #ifdef TRT_DIAG_NO_POW
-                    spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
+                    spec = 1.0f * fmaxf(0.0f, dot3(rdir, park_v())) * sexp_i; // diagnostic: prices powf
 #else
-                    spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
+                    spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, park_v())), sexp_i);
 #endif
                 }
                 // A light whose diffuse term and specular term both vanish from the colour (a
@@ -1810,12 +1854,13 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 // reference's behaviour (traces it and adds the terms when lit: its counters and
                 // image are the reference's, and tests/test_gpu_parity.py checks that its image
                 // equals the frame's bit for bit) and reports the skipped queries and their work.
-                const bool matters = TRT_SKIP_DARK == 0 || (alb[0] != 0.0f && diff != 0.0f) ||
+                const bool matters = TRT_SKIP_DARK == 0 || (alb0_i != 0.0f && diff != 0.0f) ||
                                      (alb[1] != 0.0f && spec != 0.0f);
                 if (COUNT) ++cnt.sh;
                 if (!COUNT && !matters) continue;
                 const Cnt before = cnt;
                 const bool occl = shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab);
+                if constexpr (PARK) park_fence();
                 if (COUNT && !matters) {
                     ++cnt.sk;
                     cnt.ssph += cnt.sph - before.sph;
@@ -1826,8 +1871,20 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                     cnt.stv += cnt.tv - before.tv;
                 }
                 if (occl) continue;
-                diffuse = add(diffuse, muls(kdv, diff));
-                specular = add(specular, muls(kdv, spec));
+                const f3 kd_i = park_kd();
+                diffuse = add(diffuse, muls(kd_i, diff));
+                specular = add(specular, muls(kd_i, spec));
+            }
+            if constexpr (PARK) {
+                park_fence();
+                color = mk(P[0], P[64], P[128]);
+                cur.thr = P[3 * 64];
+                cur.depth = __float_as_int(P[4 * 64]);
+                alb[2] = P[5 * 64];
+                alb[3] = P[6 * 64];
+                ior = P[7 * 64];
+                cur.d = mk(P[8 * 64], P[9 * 64], P[10 * 64]);
+                alb[0] = P[15 * 64];
             }
             color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
             // Children (shader.comp:509-575).  Children that the reference would push and
