@@ -71,7 +71,9 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=8, help="rows per band of the tiled frames")
     ap.add_argument("--frames-per-gather", type=int, default=0,
                     help="frames per RCCL exchange of the tiled loop (0 = auto: a quarter of the frames, <= 64)")
-    ap.add_argument("--camera-period", type=int, default=16, help="distinct camera positions of the walk")
+    ap.add_argument("--camera-period", type=int, default=64,
+                    help="distinct camera positions of the walk (>= the 64 frames of a launch, so no launch "
+                         "traces the same frame twice: the reference's camera never revisits a position)")
     ap.add_argument("--tiled-frames", type=int, default=20,
                     help="frames of the tiled 3840x2160 leg (C4 row-tiled + RCCL gather on rank 0); 0 skips it")
     ap.add_argument("--extra-frames", type=int, default=40,

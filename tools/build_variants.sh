@@ -30,6 +30,10 @@ for v in "$@"; do
         g3p24) variant g3p24 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=24 ;;
         g3p32) variant g3p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 ;;
         g3p16) variant g3p16 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=16 ;;
+        g3p12) variant g3p12 -DTRT_G3_LDS=12 ;;
+        swe005) variant swe005 -DTRT_SHADOW_WAVE_EXT=0.05 ;;
+        swe02) variant swe02 -DTRT_SHADOW_WAVE_EXT=0.2 ;;
+        nolp) variant nolp -DTRT_LEAF_PREFETCH=0 ;;
         g3p20) variant g3p20 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=20 ;;
         g3p28) variant g3p28 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=28 ;;
         g3w4p32) variant g3w4p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 -DTRT_G3_WAVES_SHALLOW=4 ;;
