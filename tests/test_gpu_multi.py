@@ -134,6 +134,40 @@ def test_render_multi_frames_device_batches(gpu_renderer, multi, self_gather):
         assert np.array_equal(got[i], want[i]), i
 
 
+@pytest.mark.parametrize("self_gather", [False, True])
+def test_prepared_multi_frame_list(gpu_renderer, multi, self_gather):
+    """MultiRenderer.frames_call (the bench's tiled timed loop) renders what render_frames
+    renders, re-issued twice (the batches keep alternating their slots)."""
+    torch = pytest.importorskip("torch")
+    sc = S.config_c2(160, 96, env_size=ENV)
+    ubos = _ubos(5)
+    multi.set_self_gather(self_gather)
+    multi.upload_scene(sc)
+    p = sc.params()
+    fb = p.height * p.width * 4
+    out = torch.zeros((5, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()
+    multi.set_stream(0, stream)
+    try:
+        call = multi.frames_call(p, 5, band_rows=8, root=ROOT_ROTATE, frames_per_gather=2, outs=[out],
+                                 frame_stride=fb, ubos=ubos)
+        for _ in range(2):
+            out.zero_()
+            torch.cuda.synchronize()
+            call()
+            stream.synchronize()
+            got = out.cpu().numpy()
+            want = _single_frames(gpu_renderer, sc, p, ubos)
+            for i in range(5):
+                assert np.array_equal(got[i], want[i]), i
+        with pytest.raises(ValueError):
+            multi.frames_call(p, 5, outs=[out[:2]], frame_stride=fb, ubos=ubos)
+    finally:
+        multi.set_stream(0, None)
+        multi.set_self_gather(False)
+
+
 def test_render_multi_frames_first_batches_after_upload():
     """Batches straight after an upload with the full-size envmap: the first batch (slot 0)
     builds the envmap pair rows, and the second batch's render stream (slot 1) forked before

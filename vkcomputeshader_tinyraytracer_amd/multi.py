@@ -198,6 +198,35 @@ class MultiRenderer:
             self._h, ctypes.byref(p), u.ctypes.data if u is not None else None, int(nframes), int(band_rows),
             int(root), int(frames_per_gather), arr, int(frame_stride)))
 
+    def frames_call(self, params: T.Params, nframes: int, band_rows: int = 8, root: int = 0,
+                    frames_per_gather: int = 1, outs=None, frame_stride: int = 0, ubos=None):
+        """render_frames(...) with its checks and conversions done once: a zero-argument callable
+        that only enqueues the frames (one trt_render_multi_frames call), for host loops that
+        re-issue the same frame list (every rank must issue it the same number of times)."""
+        p = T.Params.from_buffer_copy(params)
+        p.flags |= T.FLAG_DEVICE_PTRS
+        p.flags &= ~(T.FLAG_COUNT | T.FLAG_TIMING)
+        if frame_stride < 0 or frame_stride % 4:
+            raise ValueError("frame_stride must be a non-negative multiple of 4")
+        need = p.width * p.height * 4 + max(int(nframes) - 1, 0) * int(frame_stride)
+        arr = self._outs(outs, need, True)
+        u = None
+        if ubos is not None:
+            u = np.ascontiguousarray(ubos, T.UBO)
+            if u.shape[0] < nframes:
+                raise ValueError(f"{u.shape[0]} UBOs for {nframes} frames")
+        fn, h, pp = self._L.trt_render_multi_frames, self._h, ctypes.byref(p)
+        args = (u.ctypes.data if u is not None else None, int(nframes), int(band_rows), int(root),
+                int(frames_per_gather), arr, int(frame_stride))
+        keep = (p, u, arr, list(outs or []))
+
+        def call() -> None:
+            rc = fn(h, pp, *args)
+            if rc:
+                self._check(rc)
+        call.keep = keep
+        return call
+
     def synchronize(self) -> None:
         self._check(self._L.trt_multi_synchronize(self._h))
 
