@@ -778,7 +778,11 @@ def main():
                       "(-ffp-contract=off).  traffic: HBM bytes per frame of trace_kernel from PMC "
                       "(2 x FETCH_SIZE + WRITE_SIZE, see traffic_detail)")
         if not dist_mode:
-            td = measure_traffic(args, rl.get("kernel_us_per_frame"))
+            # over the kernel time per frame, or the wall time per frame when the event pass's
+            # span is not the shorter one (then the rate is a lower bound)
+            td = measure_traffic(args, rl.get("kernel_us_per_frame") or rl["us_per_frame"])
+            if td and "hbm_gb_s" in td:
+                td["time_basis"] = "kernel" if rl.get("kernel_us_per_frame") else "wall"
             if td and "bytes_per_frame" in td:
                 rl["traffic"] = td["bytes_per_frame"]
             rl["traffic_detail"] = td
