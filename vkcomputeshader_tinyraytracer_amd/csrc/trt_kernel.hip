@@ -83,6 +83,20 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
     return muls(v, inv);
 }
 __device__ __forceinline__ float length3(f3 v) { return sqrt_rn(dot3(v, v)); }
+// normalize3(v) and length3(v) of one vector with one fast-domain test (trt_math.h)
+#ifndef TRT_FUSED_NLEN
+#define TRT_FUSED_NLEN 1
+#endif
+__device__ __forceinline__ f3 normalize_len3(f3 v, float& len) {
+#if TRT_FUSED_NLEN
+    float inv;
+    len = sqrt_rsqrt_rn(dot3(v, v), inv);
+    return muls(v, inv);
+#else
+    len = length3(v);
+    return normalize3(v);
+#endif
+}
 // GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
 __device__ __forceinline__ f3 reflect3(f3 I, f3 N) {
     float k = 2.0f * dot3(N, I);
@@ -142,7 +156,8 @@ __device__ __forceinline__ f3 custom_refract(f3 I, f3 N, float eta_out, float et
     bool entering = dot3(I, N) < 0.0f;
     f3 fn = entering ? N : neg(N);
     float cosi = clamp01(dot3(neg(I), fn));
-    float eta = entering ? div_rn(eta_in, eta_out) : div_rn(eta_out, eta_in);
+    // one quotient with selected operands (the same correctly rounded value either way)
+    float eta = div_rn(entering ? eta_in : eta_out, entering ? eta_out : eta_in);
     float sint2 = eta * eta * (1.0f - cosi * cosi);
     if (sint2 > 1.0f) return mk(0.0f, 0.0f, 0.0f);
     float k = sqrt_rn(1.0f - sint2);
@@ -1667,8 +1682,7 @@ struct LightTerm {
 __device__ __forceinline__ LightTerm light_term(const KArgs& A, const Surf& s, f3 v, int i) {
     LightTerm t;
     f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
-    t.ld = normalize3(sub(L, s.p));
-    t.dist = length3(sub(L, s.p));
+    t.ld = normalize_len3(sub(L, s.p), t.dist);
     t.so = dot3(t.ld, s.n) < 0.0f ? sub(s.p, muls(s.n, TRT_EPS)) : add(s.p, muls(s.n, TRT_EPS));
     t.diff = 1.0f * fmaxf(0.0f, dot3(s.n, t.ld));
     t.spec = 0.0f; // not formed under a zero specular weight (cast_seg)
@@ -1693,8 +1707,10 @@ __device__ __forceinline__ void make_children(const Seg& cur, const Surf& s, int
     bool skip_reflect = false;
     if (s.alb[3] > 0.0f) {
         f3 rd = custom_refract(cur.d, s.n, s.ior, 1.0f);
-        if (length3(rd) > 0.0001f) {
-            rd = normalize3(rd);
+        float rl;
+        const f3 rn = normalize_len3(rd, rl);
+        if (rl > 0.0001f) {
+            rd = rn;
         } else { // total internal reflection: one reflected child, shader.comp:533-555
             rd = normalize3(reflect3(cur.d, s.n));
             skip_reflect = true;
@@ -1832,8 +1848,8 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 if constexpr (PARK) park_fence();
                 const float sexp_i = park_f(14, sexp), alb0_i = park_f(15, alb[0]);
                 f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
-                f3 ld = normalize3(sub(L, p));
-                float dist = length3(sub(L, p));
+                float dist;
+                f3 ld = normalize_len3(sub(L, p), dist);
                 f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
                 const float diff = 1.0f * fmaxf(0.0f, dot3(n, ld));
                 // With a zero specular weight (the floor, the diffuse meshes) the specular sum only
@@ -1895,8 +1911,10 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             bool skip_reflect = false;
             if (alb[3] > 0.0f) {
                 f3 rd = custom_refract(cur.d, n, ior, 1.0f);
-                if (length3(rd) > 0.0001f) {
-                    rd = normalize3(rd);
+                float rl;
+                const f3 rn = normalize_len3(rd, rl);
+                if (rl > 0.0001f) {
+                    rd = rn;
                 } else { // total internal reflection: one reflected child, shader.comp:533-555
                     rd = normalize3(reflect3(cur.d, n));
                     skip_reflect = true;

@@ -130,4 +130,30 @@ __device__ __forceinline__ float rsqrt_rn2(float x) {
 #endif
 }
 
+// sqrt(x) and 1 / sqrt(x), both correctly rounded (the contract's length(v) and normalize(v)
+// of one vector), behind one fast-domain test: s = sqrt_rn(x), r = rcp_rn(s).  On the fast
+// domain s lies in [2^-48, 2^63], inside rcp_rn_core's exact domain.
+__device__ __forceinline__ float sqrt_rsqrt_rn(float x, float& r) {
+#ifdef TRT_FM_EXEC_BRANCH
+    if (__builtin_expect(sqrt_fast_ok(x), 1)) {
+        const float s = sqrt_rn_core(x);
+        r = rcp_rn_core(s);
+        return s;
+    }
+    const float s = __builtin_sqrtf(x);
+    r = 1.0f / s;
+    return s;
+#else
+    float s = sqrt_rn_core(x);
+    float q = rcp_rn_core(s);
+    const bool ok = sqrt_fast_ok(x);
+    if (TRT_FM_RARE(ok)) {
+        s = ok ? s : __builtin_sqrtf(x);
+        q = ok ? q : 1.0f / s;
+    }
+    r = q;
+    return s;
+#endif
+}
+
 } // namespace trt
