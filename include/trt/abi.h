@@ -149,15 +149,18 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * no barrier between consecutive compute submissions).  Frame i of a trt_render_frames call
  * runs on in-flight slot i % n: slot 0 is the context's stream, slots 1..n-1 are streams the
  * context owns, forked from and joined back into its stream inside the call, so frame i+1's
- * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 8], or 0 = auto
- * (the default): 4, or 8 for deferred-shadow frames, whose depth-20 trees leave the longest
- * tails (measured: profiles/r02_ab_queues_*.log).  Each slot is a HIP stream, so the process
+ * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 32], or 0 = auto
+ * (the default): 4, or 16 for deferred-shadow frames, whose depth-20 trees leave the longest
+ * tails (measured: profiles/r02_ab_queues_*.log; 16 vs 8 in round 4: the shipped frame -16 %,
+ * the README scene -28 %, profiles/r04z_ab_deferred_in_flight.jsonl).  Each slot is a HIP stream, so the process
  * needs as many hardware queues: the library leaves GPU_MAX_HW_QUEUES to the host (HIP's
  * default is 4; the Python package and bench.py raise it to 32 before HIP initialises, see
  * INTEGRATION.md). */
 #define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
 #define TRT_FRAMES_IN_FLIGHT_AUTO 0u
-#define TRT_MAX_FRAMES_IN_FLIGHT 8u
+#ifndef TRT_MAX_FRAMES_IN_FLIGHT
+#define TRT_MAX_FRAMES_IN_FLIGHT 32u
+#endif
 int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
 
 /* Frames per launch of trt_render_frames.  The reference records one vkCmdDispatch per frame

@@ -444,7 +444,7 @@ def test_frame_batch_bounds(gpu_renderer):
     gpu_renderer.set_frame_batch(0)
 
 
-@pytest.mark.parametrize("inflight", [1, 2, 3, 4, 8, 0])
+@pytest.mark.parametrize("inflight", [1, 2, 3, 4, 8, 16, 0])
 def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
     """Frames in flight (trt_set_frames_in_flight, main.cpp:45): concurrent frames with
     distinct UBOs and images equal one-at-a-time trt_render, and all of them have landed on
@@ -475,9 +475,10 @@ def test_frames_in_flight_match_single_frames(gpu_renderer, inflight):
 
 
 def test_frames_in_flight_bounds(gpu_renderer):
-    for bad in (9, 100):
+    for bad in (33, 100):  # TRT_MAX_FRAMES_IN_FLIGHT = 32
         with pytest.raises(TrtError):
             gpu_renderer.set_frames_in_flight(bad)
+    gpu_renderer.set_frames_in_flight(32)
     gpu_renderer.set_frames_in_flight(0)
 
 

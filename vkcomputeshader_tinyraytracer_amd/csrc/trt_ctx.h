@@ -62,6 +62,7 @@ struct trt_ctx {
     uint32_t xcd_rot = trt::kDefaultXcdRot, xcd_skew = trt::kDefaultXcdSkew, xcd_inter = trt::kDefaultXcdInter;
     int frame_group = -1; // TRT_FRAME_GROUP (1 or 2); -1 = auto: 2 for triangle-free scenes, else 1
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
+    uint32_t defer_in_flight = 16; // auto frames in flight of deferred-shadow loops (TRT_DEFER_IN_FLIGHT env)
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share

@@ -221,6 +221,8 @@ int trt_create(trt_ctx** out, int hip_device) {
         return TRT_ERR_HIP;
     }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
+    if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT"))
+        c->defer_in_flight = (uint32_t)std::min((int)TRT_MAX_FRAMES_IN_FLIGHT, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_SKEW")) c->xcd_skew = (uint32_t)std::min(7, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = std::atoi(e) != 0 ? 1u : 0u;
@@ -865,9 +867,11 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     // frame against 25.0 with one launch per frame on 4 slots; at 1000 frames 15.6 vs 15.9,
     // profiles/r03_ab_frame_batch.log); with n slots set explicitly the frames are spread over
     // n launches.  Per-frame launch sequences (split / deferred-shadow frames) keep the slots
-    // busy instead: auto 4, or 8 for deferred-shadow frames (the shipped frame 1.45 -> 0.56 ms at
+    // busy instead: auto 4, or defer_in_flight (16) for deferred-shadow frames (8 vs 16 in round
+    // 4: the shipped frame 0.42 -> 0.35 ms, the README scene 0.24 -> 0.17 ms,
+    // profiles/r04z_ab_deferred_in_flight.jsonl; round 2: the shipped frame 1.45 -> 0.56 ms at
     // 8, profiles/r02_ab_queues_deep.log).
-    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : plain ? 1u : defer ? 8u : 4u;
+    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : plain ? 1u : defer ? c->defer_in_flight : 4u;
     const uint32_t cap = plain ? (c->frame_batch ? c->frame_batch : trt::kMaxLaunchFrames) : 1u;
     const uint32_t per_launch = std::max(1u, std::min(cap, (nframes + want - 1) / want));
     // launches: runs of consecutive frames sharing every UBO field but camPos

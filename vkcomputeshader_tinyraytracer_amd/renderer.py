@@ -58,7 +58,7 @@ class Renderer:
 
     def set_frames_in_flight(self, n: int) -> None:
         """Frames of render_frames that may run concurrently (trt_set_frames_in_flight; the
-        reference's MAX_FRAMES_IN_FLIGHT = 2, main.cpp:45): 1..8, or 0 = auto (4; 8 for
+        reference's MAX_FRAMES_IN_FLIGHT = 2, main.cpp:45): 1..32, or 0 = auto (4; 16 for
         deferred-shadow frames)."""
         self._check(self._L.trt_set_frames_in_flight(self._h, int(n)))
 
