@@ -76,8 +76,9 @@ def parse():
                          "traces the same frame twice: the reference's camera never revisits a position)")
     ap.add_argument("--tiled-frames", type=int, default=20,
                     help="frames of the tiled 3840x2160 leg (C4 row-tiled + RCCL gather on rank 0); 0 skips it")
-    ap.add_argument("--extra-frames", type=int, default=40,
-                    help="frames of the shipped / README-scene legs; 0 skips them")
+    ap.add_argument("--extra-frames", type=int, default=160,
+                    help="frames of the shipped / README-scene legs (16 run in flight: 160 keeps the pipeline's "
+                         "fill and drain to a few per cent); 0 skips them")
     ap.add_argument("--traffic", default="live", choices=["live", "table", "off"],
                     help="roofline.traffic: live = two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over a "
                          "child run of the same frame loop (N = 1); table = the committed measurement")
