@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--extra-frames", type=int, default=160,
                     help="frames of the shipped / README-scene legs (16 run in flight: 160 keeps the pipeline's "
                          "fill and drain to a few per cent); 0 skips them")
+    ap.add_argument("--legs", default="c3,c5,c2pf",
+                    help="extra legs (comma list; '' = none): c3 = BASELINE configs[2] (1920x1080 mesh), c5 = "
+                         "configs[4] (4K, 16 spp), c2pf = C2 at one launch per frame, 2 in flight (drawFrame)")
+    ap.add_argument("--legs-frames", type=int, default=200, help="frames of the C3 and per-frame-launch C2 legs")
+    ap.add_argument("--c5-frames", type=int, default=6, help="frames of the C5 leg (~80 ms each)")
     ap.add_argument("--traffic", default="live", choices=["live", "table", "off"],
                     help="roofline.traffic: live = two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over a "
                          "child run of the same frame loop (N = 1); table = the committed measurement")
@@ -219,10 +224,15 @@ def cpu_baseline(scene, params, rays_per_frame: int, budget_s: float) -> dict:
         return st["primary_rays"] + st["secondary_rays"], med, len(times)
 
     rays, med, n = run(hw)
+    # `cores`: the CPUs the threads could actually run on — the job's cgroup quota (16 on the GPU
+    # box) caps the 256 hardware threads of the host, so the thread count overstates the CPU
+    cores = min(hw, share)
     out = {
-        "value": round(rays / med / 1e6, 3), "unit": "Mray/s", "cores": hw, "kind": "port",
+        "value": round(rays / med / 1e6, 3), "unit": "Mray/s", "cores": cores, "threads": hw, "kind": "port",
         "sample": f"{n} whole frames of the same workload after 1 warm-up, median {med * 1e3:.1f} ms/frame; "
-                  f"oracle/trt_oracle.c fast mode, -O3, rows over {hw} threads (hardware_concurrency)",
+                  f"oracle/trt_oracle.c fast mode, -O3, pixel spans over {hw} threads (hardware_concurrency) "
+                  f"on {cores} CPUs (min of the cgroup quota {info['cgroup_cpu_quota']} and the affinity mask) of "
+                  f"a {info['model']}",
         "host": info, "rays_match_gpu": bool(rays == rays_per_frame),
     }
     if share != hw:
@@ -627,7 +637,16 @@ def _pmc_pass(counter: str, args, outdir: Path) -> list[dict]:
     return list(rows.values())
 
 
-def measure_traffic(args, kernel_us_per_frame: float | None) -> dict | None:
+def probe_args(args, **over) -> argparse.Namespace:
+    """The traffic probe's arguments: the line's own, with a leg's overrides (config, steps,
+    inflight, frame_batch, camera_period)."""
+    a = argparse.Namespace(**vars(args))
+    for k, v in over.items():
+        setattr(a, k, v)
+    return a
+
+
+def measure_traffic(args, kernel_us_per_frame: float | None, table_key: str | None = None) -> dict | None:
     """HBM bytes per frame of the dominant kernel, from two separate PMC passes (FETCH_SIZE,
     WRITE_SIZE; MI355X_MICROARCH.md §HBM: the two cannot share a pass) over a child run of the
     line's own frame loop; the launches of the timed size (the largest grid) are kept.  FETCH_SIZE
@@ -646,12 +665,16 @@ def measure_traffic(args, kernel_us_per_frame: float | None) -> dict | None:
             gmax = max(d["grid"] for d in fetch)
             f_sel = [d["value"] for d in fetch if d["grid"] == gmax]
             w_sel = [d["value"] for d in write if d["grid"] == gmax]
+            dur = [d["dur_ns"] for d in fetch + write if d["grid"] == gmax]
             frames = probe_steps(args) if args.frame_batch == 0 else min(probe_steps(args), args.frame_batch)
             fetch_b = statistics.median(f_sel) * 1024 / frames
             write_b = statistics.median(w_sel) * 1024 / frames
             out = {"source": f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over a child run of "
-                             f"this frame loop, {len(f_sel)}+{len(w_sel)} launches of {frames} frames",
-                   "fetch_bytes_raw": round(fetch_b), "write_bytes": round(write_b)}
+                             f"this frame loop ({args.config}, frame batch {args.frame_batch or 'auto'}, "
+                             f"{args.inflight or 'auto'} in flight), {len(f_sel)}+{len(w_sel)} launches of {frames} "
+                             f"frame(s)",
+                   "fetch_bytes_raw": round(fetch_b), "write_bytes": round(write_b),
+                   "launch_us_under_pmc": round(statistics.median(dur) / 1e3, 3)}
         except Exception as e:  # the committed table stands in
             out = {"live_error": f"{type(e).__name__}: {e}"}
     else:
@@ -659,7 +682,7 @@ def measure_traffic(args, kernel_us_per_frame: float | None) -> dict | None:
     if "fetch_bytes_raw" not in out:
         if not TRAFFIC_TABLE.exists():
             return out or None
-        t = json.loads(TRAFFIC_TABLE.read_text()).get(args.config)
+        t = json.loads(TRAFFIC_TABLE.read_text()).get(table_key or args.config)
         if not t:
             return out or None
         out.update({"source": f"table: {TRAFFIC_TABLE.relative_to(REPO)} ({t.get('measured', '')})",
@@ -670,6 +693,64 @@ def measure_traffic(args, kernel_us_per_frame: float | None) -> dict | None:
         out["hbm_gb_s"] = round(gbs, 1)
         out["hbm_frac"] = round(gbs / HBM_PEAK_GBS, 4)
     return out
+
+
+def attach_traffic(rl: dict, td: dict | None) -> None:
+    """roofline.traffic (+ traffic_detail) of a leg from measure_traffic."""
+    if td and "hbm_gb_s" in td:
+        td["time_basis"] = "kernel" if rl.get("kernel_us_per_frame") else "wall"
+    if td and "bytes_per_frame" in td:
+        rl["traffic"] = td["bytes_per_frame"]
+    rl["traffic_detail"] = td
+
+
+# ---- the BASELINE configs[2] / configs[4] legs and the drawFrame-paced C2 leg -----------------
+
+def config_leg(dev: int, name: str, frames: int, args, period: int) -> dict:
+    """C3 or C5 on one GPU: the plain frame loop over a camera walk of `period` positions, with
+    its roofline and live PMC traffic (BASELINE configs[2] / configs[4]; C5 is the config BASELINE
+    names for the HBM-roofline report)."""
+    a = probe_args(args, camera_period=period, inflight=0, frame_batch=0)
+    sc = make_scene(name)
+    res = frame_loop(dev, sc, frames, 2, a)
+    ms = res["elapsed"] / frames * 1e3
+    p = res["p"]
+    rl = roofline(res["mean"], ms * 1e-3, True, True, p.width * p.height, res["kernel_ms_per_frame"])
+    rl["kernel"] = "trace_kernel"
+    attach_traffic(rl, measure_traffic(probe_args(a, config=name, steps=min(frames, 64), warmup=1),
+                                       rl.get("kernel_us_per_frame") or rl["us_per_frame"]))
+    return {
+        "workload": f"{name}: {WORKLOADS[name]}; camera walk of {period} positions",
+        "frames": frames, "ms_per_frame": round(ms, 4), "fps": round(1e3 / ms, 3),
+        "mray_s": round(res["rays_total"] / res["elapsed"] / 1e6, 3),
+        "rays_per_frame": round(res["rays_total"] / frames, 1),
+        "shadow_rays_traced_per_frame": round(res["mean"]["shadow_rays"] - res["mean"]["shadow_skipped"], 1),
+        "launches": res["launches"], "last_frame_matches_trt_render": res["last_frame_ok"],
+        "roofline": rl,
+    }
+
+
+def c2_per_frame_leg(dev: int, frames: int, args) -> dict:
+    """C2 at the reference's pacing: one launch per frame (drawFrame records one vkCmdDispatch per
+    frame, main.cpp:2108-2131, 2181-2205) with MAX_FRAMES_IN_FLIGHT = 2 (main.cpp:45), beside the
+    headline's multi-frame launches."""
+    a = probe_args(args, frame_batch=1, inflight=2)
+    sc = make_scene("C2")
+    res = frame_loop(dev, sc, frames, 4, a)
+    ms = res["elapsed"] / frames * 1e3
+    p = res["p"]
+    rl = roofline(res["mean"], ms * 1e-3, True, False, p.width * p.height, res["kernel_ms_per_frame"])
+    rl["kernel"] = "trace_kernel"
+    attach_traffic(rl, measure_traffic(probe_args(a, config="C2", steps=min(frames, 64), warmup=4),
+                                       rl.get("kernel_us_per_frame") or rl["us_per_frame"], "C2_per_frame"))
+    return {
+        "workload": f"C2: {WORKLOADS['C2']}; one launch per frame, 2 frames in flight (main.cpp:45, 2181-2205)",
+        "frames": frames, "ms_per_frame": round(ms, 5), "us_per_frame": round(ms * 1e3, 3),
+        "mray_s": round(res["rays_total"] / res["elapsed"] / 1e6, 3),
+        "launches": res["launches"], "last_frame_matches_trt_render": res["last_frame_ok"],
+        "launch_span_us": round(res["kernel_ms_per_frame"] * 1e3, 3),
+        "roofline": rl,
+    }
 
 
 def main():
@@ -768,6 +849,21 @@ def main():
                     extras[key] = extra_frame(dev, name, args.extra_frames, args)
             g.barrier()
 
+    legs = [x for x in args.legs.split(",") if x] if (rank == 0 and not dist_mode) else []
+    for leg in legs:
+        key = {"c3": "c3_frame", "c5": "c5_frame", "c2pf": "c2_per_frame_launch"}.get(leg)
+        if key is None:
+            continue
+        try:
+            if leg == "c3":
+                extras[key] = config_leg(dev, "C3", args.legs_frames, args, min(args.camera_period, 64))
+            elif leg == "c5":
+                extras[key] = config_leg(dev, "C5", args.c5_frames, args, max(1, args.c5_frames))
+            else:
+                extras[key] = c2_per_frame_leg(dev, args.legs_frames, args)
+        except Exception as e:  # N = 1: report the failure in the line
+            extras[key] = {"error": f"{type(e).__name__}: {e}"}
+
     if rank == 0:
         rl = roofline(st_frame, s_frame, envmap, mesh, pixels, fl["kernel_ms_per_frame"] if not dist_mode else None)
         rl["kernel"] = "trace_kernel"
@@ -781,12 +877,7 @@ def main():
         if not dist_mode:
             # over the kernel time per frame, or the wall time per frame when the event pass's
             # span is not the shorter one (then the rate is a lower bound)
-            td = measure_traffic(args, rl.get("kernel_us_per_frame") or rl["us_per_frame"])
-            if td and "hbm_gb_s" in td:
-                td["time_basis"] = "kernel" if rl.get("kernel_us_per_frame") else "wall"
-            if td and "bytes_per_frame" in td:
-                rl["traffic"] = td["bytes_per_frame"]
-            rl["traffic_detail"] = td
+            attach_traffic(rl, measure_traffic(args, rl.get("kernel_us_per_frame") or rl["us_per_frame"]))
         result = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -158,9 +158,10 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * INTEGRATION.md). */
 #define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
 #define TRT_FRAMES_IN_FLIGHT_AUTO 0u
-#ifndef TRT_MAX_FRAMES_IN_FLIGHT
+/* Fixed by the ABI (a host cannot change it): the upper bound of n.  The library's own slot
+ * count is the private build-time TRT_BUILD_MAX_IN_FLIGHT (csrc/trt_ctx.h, default and maximum:
+ * this value); its range checks use that count. */
 #define TRT_MAX_FRAMES_IN_FLIGHT 32u
-#endif
 int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
 
 /* Frames per launch of trt_render_frames.  The reference records one vkCmdDispatch per frame
@@ -213,9 +214,25 @@ int trt_set_subtree_split(trt_ctx* ctx, int window);
 #define TRT_DEFER_ON 2
 int trt_set_deferred_shadows(trt_ctx* ctx, int mode);
 
+/* How a deferred frame is traced (all are bit-identical to the per-pixel loop):
+ * TRT_DEFER_POOL (the default): passes A/B/C as described above, a tile's lanes sharing its
+ * pending segments through an LDS pool.  TRT_DEFER_LEVELS (round 5, measured slower on the
+ * shipped frame): breadth first, one launch per tree depth over the whole frame's
+ * segments of that depth, each lane tracing one segment with its three shadow rays inline and
+ * writing a 20-byte event (colour term + child slots); pass C sums each pixel's event tree in the
+ * reference's pop order.  TRT_DEFER_LEVELS_B: the same levels without the shadow rays, which go
+ * to the dense pass B with the pool design's events.  Also settable at context creation with
+ * TRT_DEFER_MODE=pool|levels|levels_b. */
+#define TRT_DEFER_POOL 0
+#define TRT_DEFER_LEVELS 1
+#define TRT_DEFER_LEVELS_B 2
+int trt_set_defer_design(trt_ctx* ctx, int design);
+
 /* Counters of the last deferred frame rendered on `slot` (0 .. TRT_MAX_FRAMES_IN_FLIGHT-1;
- * trt_render uses one slot per stream): out[0] event chunks taken, out[1] shadow queries
- * appended, out[2] pixels re-traced in place, out[3] chunk capacity, out[4] query capacity.
+ * trt_render uses one slot per stream).  TRT_DEFER_POOL / _LEVELS_B: out[0] event chunks taken,
+ * out[1] shadow queries appended, out[2] pixels re-traced in place, out[3] chunk capacity, out[4]
+ * query capacity.  TRT_DEFER_LEVELS: out[0] events written, out[1] entries of the largest level queue,
+ * out[2] pixels re-traced in place, out[3] event capacity, out[4] entries per level queue.
  * Waits for the context's stream. */
 int trt_defer_stats(trt_ctx* ctx, uint32_t slot, uint64_t out[5]);
 

@@ -701,7 +701,7 @@ typedef struct {
     const uint32_t* rows; /* selected image rows, in output order */
     uint32_t nrows;
     float dz;
-    _Atomic uint32_t next_row;
+    _Atomic uint32_t next_item;
     uint8_t* out8;
     float* out32;
     _Atomic uint64_t acc[9];
@@ -713,12 +713,13 @@ static float srgb_encode(float x) {
     return x <= 0.0031308f ? 12.92f * x : 1.055f * powf(x, 1.0f / 2.4f) - 0.055f;
 }
 
-static void render_row(job_t* J, uint32_t k, counters* cnt, path_segment* lit_stack) {
+/* Pixels [x0, x1) of selected row k. */
+static void render_span(job_t* J, uint32_t k, uint32_t x0, uint32_t x1, counters* cnt, path_segment* lit_stack) {
     const trt_params* p = J->p;
     uint32_t y = J->rows[k], W = p->width;
     v3 orig = xyz(J->sc->ubo->camPos); /* shader.comp:595 */
     uint32_t spp = p->spp ? p->spp : 1;
-    for (uint32_t x = 0; x < W; ++x) {
+    for (uint32_t x = x0; x < x1; ++x) {
         v3 acc = mk(0, 0, 0);
         for (uint32_t s = 0; s < spp; ++s) {
             v3 d = primary_dir(p, J->dz, x, y, s);
@@ -748,16 +749,22 @@ static void render_row(job_t* J, uint32_t k, counters* cnt, path_segment* lit_st
     }
 }
 
+#define ORC_SPAN 256u /* pixels per work item */
+
 static void* worker(void* arg) {
     job_t* J = (job_t*)arg;
     counters cnt;
     memset(&cnt, 0, sizeof(cnt));
     path_segment* lit = NULL;
     if (J->mode == ORC_MODE_LITERAL) lit = (path_segment*)malloc(sizeof(path_segment) * MAX_STACK_SIZE);
+    /* work items are ORC_SPAN-pixel spans of the selected rows (rows alone leave threads idle
+     * when few long rows are selected, e.g. a handful of 4K rows at 16 spp) */
+    const uint32_t W = J->p->width, per_row = (W + ORC_SPAN - 1) / ORC_SPAN;
     for (;;) {
-        uint32_t k = atomic_fetch_add(&J->next_row, 1u);
-        if (k >= J->nrows) break;
-        render_row(J, k, &cnt, lit);
+        uint32_t i = atomic_fetch_add(&J->next_item, 1u);
+        if (i >= J->nrows * per_row) break;
+        uint32_t k = i / per_row, x0 = (i % per_row) * ORC_SPAN;
+        render_span(J, k, x0, x0 + ORC_SPAN < W ? x0 + ORC_SPAN : W, &cnt, lit);
     }
     free(lit);
     const uint64_t v[9] = {cnt.primary, cnt.secondary, cnt.shadow, cnt.miss, cnt.tri_nearest,
@@ -794,7 +801,7 @@ int orc_render(const orc_scene* sc, const trt_params* p, int mode, int nthreads,
     J.rows = rows;
     J.nrows = nrows;
     J.dz = (float)ray_dz(p);
-    atomic_init(&J.next_row, 0u);
+    atomic_init(&J.next_item, 0u);
     J.out8 = out8;
     J.out32 = out32;
     for (int i = 0; i < 9; ++i) atomic_init(&J.acc[i], 0);
@@ -803,7 +810,10 @@ int orc_render(const orc_scene* sc, const trt_params* p, int mode, int nthreads,
         nthreads = n > 0 ? (int)n : 1;
     }
     if (nthreads > 256) nthreads = 256;
-    if ((uint32_t)nthreads > nrows) nthreads = nrows ? (int)nrows : 1;
+    {
+        const uint64_t items = (uint64_t)nrows * ((p->width + ORC_SPAN - 1) / ORC_SPAN);
+        if ((uint64_t)nthreads > items) nthreads = items ? (int)items : 1;
+    }
     pthread_t th[256];
     int started = 0;
     for (int i = 1; i < nthreads; ++i)

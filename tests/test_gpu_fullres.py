@@ -7,7 +7,13 @@ a set of rows spread over the FULL frame — band_rows = 1, band_count = H / row
 i, i.e. rows i, i + band_count, ... — and the oracle (the shader.comp:338-399 restatement,
 linear batch loop) renders the same rows: 16 rows of C3 at 1920x1080, 16 rows of C4 at
 3840x2160, 4 rows of C5 at 3840x2160 and 16 spp.  Geometry counters must be equal, RGBA8
-within the parity bar (tests/helpers.py)."""
+within the parity bar (tests/helpers.py).
+
+Wider sets (round 5): one rank's share of an 8-GPU C4 frame — the interleaved 8-row bands
+band_rows = 8, band_count = 8, band_index = i, 270 of the 2,160 rows, exactly what rank i renders
+in the multi-GPU layout — and 32 spread rows of C5 at 16 spp (two sets of 16).  The
+oracle spreads its work over row spans (oracle/trt_oracle.c worker), so these take ~15-20 s each on
+the GPU box's 16-CPU share."""
 from __future__ import annotations
 
 import pytest
@@ -34,6 +40,40 @@ def test_full_resolution_rows(gpu_renderer, config, rows, index):
     o8, _, ost = orc.render(sc, p, threads=0)
     assert g8.shape == o8.shape == (len(T.output_rows(p.height, 1, count, index)), p.width, 4)
     assert g8.shape[0] >= rows
+    for k in T.Stats.EXACT:
+        assert gst[k] == ost[k], (k, gst[k], ost[k])
+    assert_rgba8_close(g8, o8)
+
+
+@pytest.mark.parametrize("index", [3])
+def test_c4_one_rank_share_of_8(gpu_renderer, index):
+    """272 rows (>= 1/8) of a C4 frame: rank `index`'s interleaved 8-row bands of an 8-GPU split."""
+    sc = S.CONFIGS["C4"]()
+    p = sc.params()
+    p.band_rows, p.band_count, p.band_index = 8, 8, index
+    gpu_renderer.upload_scene(sc)
+    g8, _, gst = gpu_renderer.draw_frame(p, count=True)
+    o8, _, ost = orc.render(sc, p, threads=0)
+    rows = T.output_rows(p.height, 8, 8, index)
+    assert len(rows) == 272 and g8.shape == o8.shape == (len(rows), p.width, 4)
+    for k in T.Stats.EXACT:
+        assert gst[k] == ost[k], (k, gst[k], ost[k])
+    assert_rgba8_close(g8, o8)
+    # the frame the plain (uncounted) launch renders is the counting pass's, bit for bit
+    g8b, _, _ = gpu_renderer.draw_frame(p)
+    assert (g8b == g8).all()
+
+
+@pytest.mark.parametrize("index", [3, 70])
+def test_c5_16_spread_rows(gpu_renderer, index):
+    """16 spread full-width rows of C5 (3840x2160, 16 jittered spp) per set; two sets = 32 rows."""
+    sc = S.CONFIGS["C5"]()
+    p = sc.params()
+    p.band_rows, p.band_count, p.band_index = 1, 135, index
+    gpu_renderer.upload_scene(sc)
+    g8, _, gst = gpu_renderer.draw_frame(p, count=True)
+    o8, _, ost = orc.render(sc, p, threads=0)
+    assert g8.shape == o8.shape == (16, p.width, 4)
     for k in T.Stats.EXACT:
         assert gst[k] == ost[k], (k, gst[k], ost[k])
     assert_rgba8_close(g8, o8)

@@ -279,6 +279,7 @@ def test_failed_batch_allocation_then_retry(gpu_renderer, monkeypatch):
     p = sc.params()
     ubos = _ubos(4)
     want = _single_frames(gpu_renderer, sc, p, ubos)
+    monkeypatch.setenv("TRT_ENABLE_TEST_HOOKS", "1")
     monkeypatch.setenv("TRT_TEST_FAIL_GROW", "3")
     m = MultiRenderer([0])
     monkeypatch.delenv("TRT_TEST_FAIL_GROW")
@@ -309,6 +310,7 @@ def test_failed_host_frame_allocation_then_retry(gpu_renderer, monkeypatch):
 
     sc = S.config_c3(160, 96, env_size=ENV)
     want, _ = _whole(gpu_renderer, sc)
+    monkeypatch.setenv("TRT_ENABLE_TEST_HOOKS", "1")
     monkeypatch.setenv("TRT_TEST_FAIL_GROW", "1")
     m = MultiRenderer([0])
     monkeypatch.delenv("TRT_TEST_FAIL_GROW")

@@ -101,7 +101,7 @@ for v in "$@"; do
         noshare) variant noshare -DTRT_SHADOW_SHARE=0 ;;
         bgearly_wpb4) variant bgearly_wpb4 -DTRT_BG_EARLY -DTRT_WPB=4 ;;
         notrig) variant notrig -DTRT_DIAG_NO_UV_TRIG ;;
-        pool64) variant pool64 -DTRT_DEFER_POOL=64 ;;
+        pool64) variant pool64 -DTRT_DEFER_POOL_N=64 ;;
         norefill) variant norefill -DTRT_DEFER_REFILL=0 ;;
         t16) variant t16 -DTRT_REFILL_T=16 ;;
         t48) variant t48 -DTRT_REFILL_T=48 ;;
@@ -109,8 +109,8 @@ for v in "$@"; do
         srefill) variant srefill -DTRT_SHADOW_REFILL=1 ;;
         dw5) variant dw5 -DTRT_DEFER_WAVES=5 ;;
         dw6) variant dw6 -DTRT_DEFER_WAVES=6 ;;
-        dw5p96) variant dw5p96 -DTRT_DEFER_WAVES=5 -DTRT_DEFER_POOL=96 ;;
-        pool192) variant pool192 -DTRT_DEFER_POOL=192 ;;
+        dw5p96) variant dw5p96 -DTRT_DEFER_WAVES=5 -DTRT_DEFER_POOL_N=96 ;;
+        pool192) variant pool192 -DTRT_DEFER_POOL_N=192 ;;
         *) echo "unknown variant $v"; exit 2 ;;
     esac
 done

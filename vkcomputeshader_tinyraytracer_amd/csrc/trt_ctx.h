@@ -12,6 +12,14 @@
 #include "../../include/trt/abi.h"
 #include "trt_device.h"
 
+// Frames-in-flight slots of a context: a private build-time knob (the public
+// TRT_MAX_FRAMES_IN_FLIGHT of abi.h is fixed and bounds it).
+#ifndef TRT_BUILD_MAX_IN_FLIGHT
+#define TRT_BUILD_MAX_IN_FLIGHT TRT_MAX_FRAMES_IN_FLIGHT
+#endif
+static_assert(TRT_BUILD_MAX_IN_FLIGHT >= 1u && TRT_BUILD_MAX_IN_FLIGHT <= TRT_MAX_FRAMES_IN_FLIGHT,
+              "TRT_BUILD_MAX_IN_FLIGHT must lie in [1, TRT_MAX_FRAMES_IN_FLIGHT]");
+
 struct trt_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -65,6 +73,10 @@ struct trt_ctx {
     uint32_t defer_in_flight = 16; // auto frames in flight of deferred-shadow loops (TRT_DEFER_IN_FLIGHT env)
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;
+    // Deferred-frame design (trt_set_defer_design): TRT_DEFER_POOL (rounds 2-4, default),
+    // TRT_DEFER_LEVELS (breadth first, inline shadow rays), TRT_DEFER_LEVELS_B (breadth first,
+    // shadow rays in pass B).  TRT_DEFER_MODE env: "pool" / "levels" / "levels_b".
+    int defer_design = TRT_DEFER_POOL;
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.
@@ -84,14 +96,25 @@ struct trt_ctx {
         uint32_t* fb = nullptr;
         trt::DeferCtr* dctr = nullptr;
         size_t ev_chunks = 0, shq_cap = 0, dnpx = 0;
+        // Level-mode deferred scratch (trt_device.h LevCtr): events (20 B each), the two level
+        // queues (32 B per entry), per-pixel fallback flags, the counters.
+        float4* lv_ev = nullptr;
+        uint32_t* lv_evr = nullptr;
+        float4* lv_q[2] = {nullptr, nullptr};
+        uint32_t* lv_qlink[2] = {nullptr, nullptr};
+        trt::LevCtr* lv_ctr = nullptr;
+        uint32_t* lv_flag = nullptr;
+        size_t lv_evcap = 0, lv_qcap = 0, lv_npx = 0;
+        bool last_levels = false; // the slot's last deferred frame ran TRT_DEFER_LEVELS
+        size_t last_npx = 0;
         // The stream of the slot's last frame and an event after it: a frame on another
         // stream waits for it before reusing the scratch (trt_render on alternating
         // streams, e.g. dist.PipelinedTiles, must not race on the task queues).
         hipStream_t last = nullptr;
         hipEvent_t done = nullptr;
     };
-    SplitBufs split[TRT_MAX_FRAMES_IN_FLIGHT];
-    hipStream_t render_slot_stream[TRT_MAX_FRAMES_IN_FLIGHT] = {}; // trt_render: stream -> slot (LRU)
+    SplitBufs split[TRT_BUILD_MAX_IN_FLIGHT];
+    hipStream_t render_slot_stream[TRT_BUILD_MAX_IN_FLIGHT] = {}; // trt_render: stream -> slot (LRU)
     uint32_t render_slot_next = 0;
     std::vector<hipStream_t> aux; // frames-in-flight streams (frame i -> stream i % n)
     std::vector<hipEvent_t> aux_ev;

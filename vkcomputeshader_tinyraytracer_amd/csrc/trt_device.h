@@ -193,6 +193,23 @@ struct DeferCtr {
     uint32_t nq[kDeferStripes * kCtrStride];       // [s * kCtrStride]: queries appended to stripe s
 };
 
+// Deferred frame, LEVEL mode (round 5, trt_kernel.hip level_kernel): the frame's segments are
+// traced breadth first, one launch per tree depth.  Level 0 is the primary rays (one lane per
+// pixel, 8x8 tiles); the children a level makes are appended to the next level's queue, so every
+// launch traces full waves of segments of ONE depth instead of a tile's lanes waiting for its
+// deepest pixel.  Shadow rays are traced inline, so a segment's colour term is final when its
+// event is written: an event is 20 B (term rgb + reflection child slot, and the refraction child
+// slot), where the pool design logged kd, diffuse / specular terms and weights (64 B) plus a 32-B
+// shadow query per light.  Event slots are implicit: level-0 segment of compact pixel o has slot
+// o; level k >= 1 entry i has slot base_k + i, base_1 = npx, base_{k+1} = base_k + n_k, so a
+// parent knows its children's slots when it queues them.  Pass C walks each pixel's tree in the
+// reference's pop order (node, reflection subtree, refraction subtree: shader.comp:530-575).
+// Queue entry: 2 x float4 = (o.xyz, d.x), (d.y, d.z, thr, output pixel).
+struct LevCtr {
+    uint32_t n[(kMaxTreeDepth + 1u) * kCtrStride];    // [k * kCtrStride]: entries appended to level k's queue
+    uint32_t take[(kMaxTreeDepth + 1u) * kCtrStride]; // [k * kCtrStride]: 64-entry chunks taken from it
+};
+
 struct SphereArg {
     float c[3];
     float r;
@@ -282,6 +299,17 @@ struct KArgs {
     uint2* __restrict__ px_ev;        // per output pixel: (root event slot or kEvNone, 0)
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
+    // deferred frames, level mode (lv != 0): see LevCtr
+    uint32_t lv;                      // level mode: 1 = shadow rays inline, 2 = shadows in pass B
+    uint32_t lv_level;                // the depth this launch traces (level_kernel)
+    uint32_t lv_qcap;                 // entries per level queue
+    uint32_t lv_evcap;                // event slots
+    float4* __restrict__ lv_ev;       // per event slot: term rgb, reflection child slot (kEvNone: none)
+    uint32_t* __restrict__ lv_evr;    // per event slot: refraction child slot
+    float4* __restrict__ lv_q[2];     // level k's queue: lv_q[k & 1], 2 float4 per entry
+    uint32_t* __restrict__ lv_qlink[2]; // lv == 2: per entry, its parent link (slot << 1 | refraction)
+    LevCtr* __restrict__ lv_ctr;
+    uint32_t* __restrict__ lv_flag;   // per compact pixel: 1 = handed to defer_fallback
     FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch
 };
 static_assert(sizeof(KArgs) <= 4096, "KArgs fits the 4 KB kernel-argument limit");

@@ -1973,10 +1973,10 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
 // while the others idle (round 3: 19.6 of 64 lanes active in pass A of the shipped frame).
 // When the pool is full a child goes to the lane's private overflow stack (<= MAX_DEPTH - 1
 // entries: their depths increase from bottom to top).
-#ifndef TRT_DEFER_POOL
-#define TRT_DEFER_POOL 128
+#ifndef TRT_DEFER_POOL_N
+#define TRT_DEFER_POOL_N 128
 #endif
-constexpr uint32_t kPool = TRT_DEFER_POOL;
+constexpr uint32_t kPool = TRT_DEFER_POOL_N;
 constexpr int kPoolFields = 10; // o.xyz, d.xyz, thr, depth, parent link, pixel
 constexpr int defer_pool_floats() { return (int)kPool * kPoolFields; }
 
@@ -3016,6 +3016,309 @@ static uint32_t defer_stages() { // debug: TRT_DEFER_STAGES bitmask of passes to
     return e ? (uint32_t)strtoul(e, nullptr, 0) : 0xFFu;
 }
 
+// ---- deferred frame, level mode (trt_device.h LevCtr) --------------------------------------
+//
+// One launch per depth of the frame's segment trees.  Each lane traces ONE segment: its closest
+// hit, its Phong terms with their shadow rays traced inline (shader.comp:483-507; a wave's lanes
+// query the same light at the same time, from neighbouring points at low depths, so the
+// wave-coherent shadow walk applies), its colour term, and its children (shader.comp:509-575),
+// which go to the next level's queue.  Why: in the pool design (defer_walk) a tile's wave
+// carried every segment of its 64 pixels' trees, so a glass tile ran for its deepest pixel's
+// chain while other tiles idled, and the frame's latency was its slowest tile; here every
+// launch spreads one depth's segments of the whole frame over the GPU in full waves.
+#ifndef TRT_LV_WAVES
+#define TRT_LV_WAVES 4
+#endif
+#ifndef TRT_LV_WPC
+#define TRT_LV_WPC 8 /* level_kernel grid: workgroups (one wave each) per CU */
+#endif
+
+// The pixel goes to defer_fallback (once): a child that did not fit the level queue or the
+// event slots.
+__device__ __forceinline__ void lv_mark(const KArgs& A, uint32_t pix) {
+    if (atomicExch(&A.lv_flag[pix], 1u) == 0u) A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
+}
+
+// One segment of level `lvl`: closest hit, colour term with inline shadow rays, children.  Every
+// lane of the wave calls it (the child append is wave-aggregated); `valid` lanes hold a segment.
+// `slot`: its event slot; `nbase`: the first event slot of level lvl + 1.
+template <int GEOM>
+__device__ __forceinline__ void lv_segment(const KArgs& A, bool valid, Seg cur, uint32_t pix, uint32_t slot,
+                                           uint32_t lvl, uint32_t nbase, float4* slab) {
+    Cnt cnt;
+    f3 term = mk(0.0f, 0.0f, 0.0f);
+    bool mk_refl = false, mk_refr = false;
+    Seg refl, refr;
+    if (valid) {
+        Hit h;
+        scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
+        if (h.kind == HIT_NONE) {
+            term = muls(background(A, cur.d), cur.thr); // shader.comp:455-458
+        } else {
+            const Surf sf = resolve_hit<false>(A, cur, h, cnt);
+            const f3 v = neg(cur.d);
+            const f3 kdv = mk(sf.kd[0], sf.kd[1], sf.kd[2]);
+            f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { // shader.comp:491-505
+                const LightTerm t = light_term(A, sf, v, i);
+                if (!t.matters) continue;
+                if (shadow_intersect<false, GEOM>(A, t.so, t.ld, t.dist, cnt, slab)) continue;
+                diffuse = add(diffuse, muls(kdv, t.diff));
+                specular = add(specular, muls(kdv, t.spec));
+            }
+            term = muls(add(muls(diffuse, sf.alb[0]), muls(specular, sf.alb[1])), cur.thr);
+            make_children(cur, sf, (int)A.max_depth, refr, mk_refr, refl, mk_refl);
+        }
+    }
+    // children to level lvl + 1: the wave's reflection children, then its refraction children
+    uint32_t srefl = kEvNone, srefr = kEvNone;
+    const uint64_t ba = __ballot(mk_refl), bb = __ballot(mk_refr);
+    if ((ba | bb) != 0ull) {
+        const uint32_t na = (uint32_t)__popcll(ba), nb = (uint32_t)__popcll(bb);
+        uint32_t q0 = 0;
+        if (lane_id() == 0u) q0 = atomicAdd(&A.lv_ctr->n[(lvl + 1u) * kCtrStride], na + nb);
+        q0 = __shfl(q0, 0, 64);
+        float4* Q = A.lv_q[(lvl + 1u) & 1u];
+        bool ovf = false;
+        auto put = [&](bool f, uint32_t i, const Seg& x, uint32_t& sl) {
+            if (!f) return;
+            if (i >= A.lv_qcap || nbase + i >= A.lv_evcap) {
+                ovf = true;
+                return;
+            }
+            Q[2 * (size_t)i] = make_float4(x.o.x, x.o.y, x.o.z, x.d.x);
+            Q[2 * (size_t)i + 1] = make_float4(x.d.y, x.d.z, x.thr, __uint_as_float(pix));
+            sl = nbase + i;
+        };
+        put(mk_refl, q0 + lane_rank(ba), refl, srefl);
+        put(mk_refr, q0 + na + lane_rank(bb), refr, srefr);
+        if (ovf) lv_mark(A, pix);
+    }
+    if (valid) {
+        A.lv_ev[slot] = make_float4(term.x, term.y, term.z, __uint_as_float(srefl));
+        A.lv_evr[slot] = srefr;
+    }
+}
+
+// Entries of a level queue that were written: a parent queues a child only when its entry
+// index fits the queue and its event slot fits the event slots (lv_segment), so of the n
+// requested entries of a level whose first event slot is `base`, min(n, qcap, evcap - base)
+// exist.  Level k's base is npx plus the earlier levels' written entries.
+__device__ __forceinline__ uint32_t lv_written(const KArgs& A, uint32_t n, uint32_t base) {
+    n = min(n, A.lv_qcap);
+    return base >= A.lv_evcap ? 0u : min(n, A.lv_evcap - base);
+}
+// (level lvl's written entries, its first event slot)
+__device__ __forceinline__ uint2 lv_level_range(const KArgs& A, uint32_t lvl) {
+    const LevCtr* C = A.lv_ctr;
+    uint32_t base = A.rows * A.width;
+    for (uint32_t j = 1u; j < lvl; ++j) base += lv_written(A, C->n[j * kCtrStride], base);
+    return make_uint2(lv_written(A, C->n[lvl * kCtrStride], base), base);
+}
+
+// Level 0: the primary rays, one 8x8 tile per wave (xcd_tile dealing, as trace_kernel).
+template <int GEOM>
+__global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level0(KArgs A) {
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    const uint32_t tile = xcd_tile(A, blockIdx.x), lane = lane_id();
+    if (tile >= A.ntiles) return;
+    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
+    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    const bool valid = x < A.width && k < A.rows;
+    const FrameRec& F = A.fr[0];
+    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
+    const uint32_t o = valid ? k * A.width + x : 0u;
+    const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
+    lv_segment<GEOM>(A, valid, root, o, o, 0u, A.rows * A.width, slab);
+}
+
+// Level lvl >= 1: waves take 64-entry chunks of the level's queue until it is drained.
+template <int GEOM>
+__global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level(KArgs A) {
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    const uint32_t lvl = A.lv_level;
+    const uint2 nb = lv_level_range(A, lvl);
+    const uint32_t n = nb.x, base = nb.y; // written entries, first event slot of this level
+    if (n == 0u) return;
+    const float4* Q = A.lv_q[lvl & 1u];
+    for (;;) {
+        uint32_t c = 0;
+        if (lane_id() == 0u) c = atomicAdd(&A.lv_ctr->take[lvl * kCtrStride], 1u);
+        c = __shfl(c, 0, 64);
+        if (c * 64u >= n) break;
+        const uint32_t i = c * 64u + lane_id();
+        const bool valid = i < n;
+        Seg cur{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f), 0.0f, (int)lvl};
+        uint32_t pix = 0;
+        if (valid) {
+            const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
+            cur.o = mk(a.x, a.y, a.z);
+            cur.d = mk(a.w, b.x, b.y);
+            cur.thr = b.z;
+            pix = __float_as_uint(b.w);
+        }
+        lv_segment<GEOM>(A, valid, cur, pix, base + i, lvl, base + n, slab);
+    }
+}
+
+// Level mode 2: the same levels with the shadow rays deferred to pass B (defer_shadows) and the
+// pool design's events (defer_shade: kd, terms and weights, 64 B) at implicit slots, so a
+// level's critical path is its closest-hit walks only.  A segment's children go to the next
+// level's queue with their parent links; defer_shade links each event into its parent's.
+template <int GEOM>
+__device__ __forceinline__ void lvb_segment(const KArgs& A, bool valid, Seg cur, uint32_t pix, uint32_t link,
+                                            uint32_t slot, uint32_t lvl, uint32_t nbase, uint32_t stripe,
+                                            float4* slab) {
+    Cnt cnt;
+    bool have = false, have_other = false;
+    PSeg other;
+    EvLog L;
+    L.stripe = stripe;
+    if (valid) {
+        Hit h;
+        scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
+        defer_shade<false>(A, L, slot, h, cur, link, pix, have, other, have_other);
+    }
+    // children to level lvl + 1 (defer_shade left the first in cur / link, the second in other)
+    const uint64_t ba = __ballot(have), bb = __ballot(have_other);
+    if ((ba | bb) != 0ull) {
+        const uint32_t na = (uint32_t)__popcll(ba), nb = (uint32_t)__popcll(bb);
+        uint32_t q0 = 0;
+        if (lane_id() == 0u) q0 = atomicAdd(&A.lv_ctr->n[(lvl + 1u) * kCtrStride], na + nb);
+        q0 = __shfl(q0, 0, 64);
+        float4* Q = A.lv_q[(lvl + 1u) & 1u];
+        uint32_t* QL = A.lv_qlink[(lvl + 1u) & 1u];
+        bool ovf = false;
+        auto put = [&](bool f, uint32_t i, const Seg& x, uint32_t lk) {
+            if (!f) return;
+            if (i >= A.lv_qcap || nbase + i >= A.lv_evcap) {
+                ovf = true;
+                return;
+            }
+            Q[2 * (size_t)i] = make_float4(x.o.x, x.o.y, x.o.z, x.d.x);
+            Q[2 * (size_t)i + 1] = make_float4(x.d.y, x.d.z, x.thr, __uint_as_float(pix));
+            QL[i] = lk;
+        };
+        put(have, q0 + lane_rank(ba), cur, link);
+        put(have_other, q0 + na + lane_rank(bb), other.s, other.link);
+        if (ovf) defer_mark_fallback(A, pix);
+    }
+}
+
+template <int GEOM>
+__global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level0(KArgs A) {
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    const uint32_t tile = xcd_tile(A, blockIdx.x), lane = lane_id();
+    if (tile >= A.ntiles) return;
+    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
+    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    const bool valid = x < A.width && k < A.rows;
+    const FrameRec& F = A.fr[0];
+    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
+    const uint32_t o = valid ? k * A.width + x : 0u;
+    const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
+    const uint32_t stripe = (tile * 0x9E3779B1u) >> (32 - 7);
+    lvb_segment<GEOM>(A, valid, root, o, kEvRoot, o, 0u, A.rows * A.width, stripe, slab);
+}
+
+template <int GEOM>
+__global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level(KArgs A) {
+    __shared__ float4 slab[slab_float4s<GEOM>()];
+    const uint32_t lvl = A.lv_level;
+    const uint2 nb = lv_level_range(A, lvl);
+    const uint32_t n = nb.x, base = nb.y;
+    if (n == 0u) return;
+    const float4* Q = A.lv_q[lvl & 1u];
+    const uint32_t* QL = A.lv_qlink[lvl & 1u];
+    for (;;) {
+        uint32_t c = 0;
+        if (lane_id() == 0u) c = atomicAdd(&A.lv_ctr->take[lvl * kCtrStride], 1u);
+        c = __shfl(c, 0, 64);
+        if (c * 64u >= n) break;
+        const uint32_t i = c * 64u + lane_id();
+        const bool valid = i < n;
+        Seg cur{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f), 0.0f, (int)lvl};
+        uint32_t pix = 0, link = kEvRoot;
+        if (valid) {
+            const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
+            cur.o = mk(a.x, a.y, a.z);
+            cur.d = mk(a.w, b.x, b.y);
+            cur.thr = b.z;
+            pix = __float_as_uint(b.w);
+            link = QL[i];
+        }
+        const uint32_t stripe = ((c + 0x5bd1e995u * lvl) * 0x9E3779B1u) >> (32 - 7);
+        lvb_segment<GEOM>(A, valid, cur, pix, link, base + i, lvl, base + n, stripe, slab);
+    }
+}
+
+// Pass C of a level-mode frame: each pixel's terms summed in the reference's pop order
+// (shader.comp:530-575), then clamp, gamma and the dual store.  Pixels handed to the fallback
+// are skipped.
+__global__ __launch_bounds__(64) void lv_resolve(KArgs A) {
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
+    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    if (x >= A.width || k >= A.rows) return;
+    const uint32_t o = k * A.width + x;
+    if (A.lv_flag[o]) return;
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    uint32_t stk[kMaxTreeDepth]; // pending refraction subtrees, one per depth of the path
+    uint32_t s = o, sp = 0, steps = 0;
+    for (;;) {
+        // a tree has at most 2^MAX_DEPTH - 1 events: a corrupt log must not hang the GPU
+        if (++steps > (1u << kMaxTreeDepth) || s >= A.lv_evcap) {
+            color = mk(1.0f, 0.0f, 1.0f);
+            break;
+        }
+        const float4 e = A.lv_ev[s];
+        color = add(color, mk(e.x, e.y, e.z));
+        const uint32_t refl = __float_as_uint(e.w), refr = A.lv_evr[s];
+        if (refl != kEvNone) {
+            if (refr != kEvNone && sp < kMaxTreeDepth) stk[sp++] = refr;
+            s = refl;
+        } else if (refr != kEvNone) {
+            s = refr;
+        } else if (sp > 0u) {
+            s = stk[--sp];
+        } else {
+            break;
+        }
+    }
+    store_pixel(A, A.fr[0], o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
+}
+
+template <int CAP, int GEOM>
+static void launch_levels(const KArgs& A0, hipStream_t stream, dim3 grid) {
+    KArgs A = A0;
+    const uint32_t stages = defer_stages();
+    if (A.lv == 2) { // shadow rays deferred: the levels, then passes B and C of the pool design
+        if (stages & 1) hipLaunchKernelGGL(lvb_level0<GEOM>, grid, dim3(64), 0, stream, A);
+        for (uint32_t k = 1; k < A.max_depth && (stages & 2); ++k) {
+            A.lv_level = k;
+            hipLaunchKernelGGL(lvb_level<GEOM>, dim3(A.num_cus * TRT_LV_WPC), dim3(64), 0, stream, A);
+        }
+        if (stages & 4)
+            hipLaunchKernelGGL(defer_shadows<GEOM>,
+                               dim3(((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes), dim3(64), 0,
+                               stream, A);
+        if (stages & 8) hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
+        if (stages & 16)
+            hipLaunchKernelGGL((defer_fallback<CAP, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
+        return;
+    }
+    if (stages & 1) hipLaunchKernelGGL(lv_level0<GEOM>, grid, dim3(64), 0, stream, A);
+    for (uint32_t k = 1; k < A.max_depth && (stages & 2); ++k) {
+        A.lv_level = k;
+        hipLaunchKernelGGL(lv_level<GEOM>, dim3(A.num_cus * TRT_LV_WPC), dim3(64), 0, stream, A);
+    }
+    if (stages & 8) hipLaunchKernelGGL(lv_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
+    if (stages & 16)
+        hipLaunchKernelGGL((defer_fallback<CAP, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
+}
+
+
 #ifndef TRT_DEFER_LDS
 #define TRT_DEFER_LDS 3 /* deferred refraction children of a deep deferred frame kept in LDS */
 #endif
@@ -3115,6 +3418,20 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const dim3 grid(A.ntiles), block(64);
 #endif
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
+    if (A.defer && A.lv && !count && A.spp <= 1 && A.dctr && A.fb && A.lv_q[0] && A.lv_q[1] && A.lv_ctr &&
+        (A.lv == 2 ? (A.ev && A.shq && A.px_ev && A.lv_qlink[0] && A.lv_qlink[1]) : (A.lv_ev && A.lv_evr && A.lv_flag))) {
+        // level mode: memsets of the counters (and the inline design's fallback flags), then the levels
+        hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
+        if (e == hipSuccess) e = hipMemsetAsync(A.lv_ctr, 0, sizeof(LevCtr), stream);
+        if (e == hipSuccess && A.lv == 1) e = hipMemsetAsync(A.lv_flag, 0, (size_t)A.rows * A.width * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        // the fallback runs the per-pixel loop with the full-depth private stack
+        if (geom == 0) launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 0>(A, stream, grid);
+        else if (geom == 1) launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 1>(A, stream, grid);
+        else if (geom == 2) launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 2>(A, stream, grid);
+        else launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 3>(A, stream, grid);
+        return hipGetLastError();
+    }
     if (A.defer && !count && A.spp <= 1 && A.dctr && A.ev && A.shq && A.px_ev && A.fb) {
         hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
         if (e == hipSuccess && A.split_w >= 1 && A.ctr) e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);

@@ -85,6 +85,16 @@ struct trt_multi {
 
 namespace {
 
+// Failure injection (tests only): TRT_TEST_FAIL_GROW=k makes the k-th buffer growth of a new
+// context fail, but only together with the test-only switch TRT_ENABLE_TEST_HOOKS=1, so a
+// deployment that happens to set the first variable gets no injected failures.
+uint32_t test_fail_grow_at() {
+    const char* on = std::getenv("TRT_ENABLE_TEST_HOOKS");
+    if (!on || std::strcmp(on, "1") != 0) return 0;
+    const char* e = std::getenv("TRT_TEST_FAIL_GROW");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+}
+
 constexpr size_t kScratchBytes = 4096;
 static_assert(sizeof(trt::SceneHeader) <= kScratchBytes, "scene header fits the scratch buffer");
 
@@ -457,7 +467,7 @@ int trt_multi_create(trt_multi** out, const int* devices, uint32_t ndev) {
     if (!devices || ndev == 0) return TRT_ERR_INVALID;
     trt_multi* m = new (std::nothrow) trt_multi();
     if (!m) return TRT_ERR_OOM;
-    if (const char* e = std::getenv("TRT_TEST_FAIL_GROW")) m->fail_grow_at = (uint32_t)std::strtoul(e, nullptr, 10);
+    m->fail_grow_at = test_fail_grow_at();
     m->nranks = ndev;
     m->devs.resize(ndev);
     std::vector<ncclComm_t> comms(ndev, nullptr);
@@ -493,7 +503,7 @@ int trt_multi_create_rank(trt_multi** out, int device, uint32_t nranks, uint32_t
     if (!id || nranks == 0 || rank >= nranks) return TRT_ERR_INVALID;
     trt_multi* m = new (std::nothrow) trt_multi();
     if (!m) return TRT_ERR_OOM;
-    if (const char* e = std::getenv("TRT_TEST_FAIL_GROW")) m->fail_grow_at = (uint32_t)std::strtoul(e, nullptr, 10);
+    m->fail_grow_at = test_fail_grow_at();
     m->nranks = nranks;
     m->devs.resize(1);
     m->devs[0].device = device;

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
+#include <cstdio>
 #include <cstdlib>
 #include <limits>
 #include <cstring>
@@ -207,8 +208,8 @@ int trt_create(trt_ctx** out, int hip_device) {
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc((void**)&c->d_counters, 32 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&c->d_persist, kPersistWords * TRT_MAX_FRAMES_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(c->d_persist, 0, kPersistWords * TRT_MAX_FRAMES_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc((void**)&c->d_persist, kPersistWords * TRT_BUILD_MAX_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(c->d_persist, 0, kPersistWords * TRT_BUILD_MAX_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess) {
         trt_destroy(c);
         return TRT_ERR_HIP;
     }
@@ -221,8 +222,11 @@ int trt_create(trt_ctx** out, int hip_device) {
         return TRT_ERR_HIP;
     }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
+    if (const char* e = std::getenv("TRT_DEFER_MODE"))
+        c->defer_design = std::strcmp(e, "levels") == 0 ? TRT_DEFER_LEVELS
+                          : std::strcmp(e, "levels_b") == 0 ? TRT_DEFER_LEVELS_B : TRT_DEFER_POOL;
     if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT"))
-        c->defer_in_flight = (uint32_t)std::min((int)TRT_MAX_FRAMES_IN_FLIGHT, std::max(1, std::atoi(e)));
+        c->defer_in_flight = (uint32_t)std::min((int)TRT_BUILD_MAX_IN_FLIGHT, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_SKEW")) c->xcd_skew = (uint32_t)std::min(7, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = std::atoi(e) != 0 ? 1u : 0u;
@@ -282,7 +286,7 @@ int trt_set_stream(trt_ctx* c, void* s) {
 
 int trt_set_frames_in_flight(trt_ctx* c, uint32_t n) {
     if (!c) return TRT_ERR_INVALID;
-    if (n > TRT_MAX_FRAMES_IN_FLIGHT)
+    if (n > TRT_BUILD_MAX_IN_FLIGHT)
         return fail(c, TRT_ERR_INVALID, "trt_set_frames_in_flight: n must be 0 (auto) or in [1, TRT_MAX_FRAMES_IN_FLIGHT]");
     c->frames_in_flight = n;
     return TRT_OK;
@@ -304,9 +308,18 @@ int trt_set_deferred_shadows(trt_ctx* c, int mode) {
     return TRT_OK;
 }
 
+int trt_set_defer_design(trt_ctx* c, int design) {
+    if (!c) return TRT_ERR_INVALID;
+    if (design != TRT_DEFER_POOL && design != TRT_DEFER_LEVELS && design != TRT_DEFER_LEVELS_B)
+        return fail(c, TRT_ERR_INVALID,
+                    "trt_set_defer_design: design must be TRT_DEFER_POOL, TRT_DEFER_LEVELS or TRT_DEFER_LEVELS_B");
+    c->defer_design = design;
+    return TRT_OK;
+}
+
 int trt_defer_stats(trt_ctx* c, uint32_t slot, uint64_t out[5]) {
     if (!c || !out) return TRT_ERR_INVALID;
-    if (slot >= TRT_MAX_FRAMES_IN_FLIGHT) return fail(c, TRT_ERR_INVALID, "trt_defer_stats: slot out of range");
+    if (slot >= TRT_BUILD_MAX_IN_FLIGHT) return fail(c, TRT_ERR_INVALID, "trt_defer_stats: slot out of range");
     const auto& b = c->split[slot];
     for (int i = 0; i < 5; ++i) out[i] = 0;
     if (!b.dctr) return TRT_OK;
@@ -315,6 +328,24 @@ int trt_defer_stats(trt_ctx* c, uint32_t slot, uint64_t out[5]) {
     if (b.last && b.done) HIP_TRY(c, hipEventSynchronize(b.done));
     trt::DeferCtr d{};
     HIP_TRY(c, hipMemcpy(&d, b.dctr, sizeof(d), hipMemcpyDeviceToHost));
+    if (b.last_levels) { // the slot's last deferred frame ran the level design
+        trt::LevCtr lc{};
+        HIP_TRY(c, hipMemcpy(&lc, b.lv_ctr, sizeof(lc), hipMemcpyDeviceToHost));
+        uint64_t ev = b.last_npx, big = 0; // written entries as the kernel counts them (lv_written)
+        for (uint32_t k = 1; k <= trt::kMaxTreeDepth; ++k) {
+            const uint64_t n = lc.n[k * trt::kCtrStride];
+            const uint64_t w = ev >= b.lv_evcap ? 0 : std::min<uint64_t>(std::min<uint64_t>(n, b.lv_qcap), b.lv_evcap - ev);
+            ev += w;
+            big = std::max<uint64_t>(big, n);
+            if (std::getenv("TRT_LV_DEBUG")) std::fprintf(stderr, "trt: level %u: %llu entries\n", k, (unsigned long long)n);
+        }
+        out[0] = ev;
+        out[1] = big;
+        out[2] = d.nfb;
+        out[3] = b.lv_evcap;
+        out[4] = b.lv_qcap;
+        return TRT_OK;
+    }
     const size_t ev_s = b.ev_chunks / trt::kDeferStripes, q_s = b.shq_cap / trt::kDeferStripes;
     for (uint32_t s = 0; s < trt::kDeferStripes; ++s) { // taken = min(requested, stripe capacity)
         out[0] += std::min<size_t>(d.chunks[s * trt::kCtrStride], ev_s);
@@ -689,53 +720,172 @@ size_t env_cap(const char* name, size_t v) {
     return v;
 }
 
-// Allocates slot `slot`'s deferred-shadow scratch for this frame and fills A's defer fields.
+// ---- deferred-frame scratch (one set per frames-in-flight slot) ----------------------------
+
+// Pool-design sizes (and the pass-B query queue of TRT_DEFER_LEVELS_B): event chunks (per tile:
+// ceil((2^D - 1) / kEvRows) at depth <= 4, else 4 on average, at least 128 per stripe) and
+// shadow queries (6 per pixel on average), both split into kDeferStripes equal stripes (tile t
+// uses stripe hash(t)); ~1.2 KB per pixel at depth >= 5 (16 events of 64 B + 6 queries of 32 B).
+// Every lane of a pool wave takes an event slot on every step of the wave's shared segment pool
+// (idle lanes too, so the lanes stay on one row of one chunk), so a tile's event count is set by
+// the pool's schedule, not bounded by 2^D - 1 per pixel; a tile that runs out re-traces its
+// pixels in place (defer_fallback: the image stays exact, only slower).  Slot ids
+// (chunk * kEvRows + row) * 64 + lane travel in 30 bits of a query.
+constexpr size_t kPoolEvBytes = trt::kEvRows * 4 * 64 * sizeof(float4); // one chunk
+size_t pool_chunks(size_t ntiles, uint32_t D) {
+    const size_t per_tile = D <= 4 ? ((1u << D) - 1u + trt::kEvRows - 1u) / trt::kEvRows : 4u;
+    constexpr size_t S = trt::kDeferStripes;
+    const size_t tiles_per_stripe = (ntiles + S - 1) / S;
+    return S * std::min<size_t>(std::max<size_t>(tiles_per_stripe * per_tile, D <= 4 ? 16u : 128u),
+                                (1u << 30) / (trt::kEvRows * 64u) / S);
+}
+size_t shadow_qcap(size_t ntiles) {
+    constexpr size_t S = trt::kDeferStripes;
+    const size_t tiles_per_stripe = (ntiles + S - 1) / S;
+    return S * std::min<size_t>(std::max<size_t>(6 * tiles_per_stripe * 64u, 1u << 12), 0xFFFFFFFFu / S);
+}
+// Level designs: kLvEvPerPixel event slots per pixel on average (the shipped frame logs 1.9) and
+// one queue entry per pixel per level (a level with more children than the frame has pixels
+// hands the rest to the fallback).
+constexpr size_t kLvEvPerPixel = 4;
+
+struct DeferSizes {
+    size_t chunks = 0, qcap = 0;           // pool-format events (chunks) and shadow queries
+    size_t lv_evcap = 0, lv_qcap = 0;      // TRT_DEFER_LEVELS events / either level design's queues
+    bool links = false;                    // TRT_DEFER_LEVELS_B: queue entries carry parent links
+    size_t bytes = 0;
+};
+DeferSizes defer_sizes(int design, size_t ntiles, uint32_t D, size_t npx) {
+    DeferSizes z;
+    if (design == TRT_DEFER_POOL) {
+        z.chunks = pool_chunks(ntiles, D);
+        z.qcap = shadow_qcap(ntiles);
+    } else {
+        z.lv_qcap = std::min<size_t>(npx, 0x7FFFFFFFu);
+        if (design == TRT_DEFER_LEVELS) {
+            z.lv_evcap = std::min<size_t>(npx * kLvEvPerPixel, 0xFFFFFFF0u);
+        } else {
+            constexpr size_t S = trt::kDeferStripes, slots = trt::kEvRows * 64u;
+            const size_t want = std::min<size_t>(npx * kLvEvPerPixel, (1u << 30) - 1u);
+            z.chunks = ((want + slots - 1) / slots + S - 1) / S * S;
+            z.qcap = shadow_qcap(ntiles);
+            z.links = true;
+        }
+    }
+    z.bytes = z.chunks * kPoolEvBytes + z.qcap * 2 * sizeof(float4) +
+              z.lv_evcap * (sizeof(float4) + sizeof(uint32_t)) +
+              2 * z.lv_qcap * (2 * sizeof(float4) + (z.links ? sizeof(uint32_t) : 0)) +
+              npx * (sizeof(uint2) + 2 * sizeof(uint32_t)) + sizeof(trt::LevCtr) + sizeof(trt::DeferCtr);
+    return z;
+}
+
+bool defer_bufs_fit(const trt_ctx::SplitBufs& b, const DeferSizes& z, size_t npx) {
+    return z.chunks <= b.ev_chunks && z.qcap <= b.shq_cap && z.lv_evcap <= b.lv_evcap && z.lv_qcap <= b.lv_qcap &&
+           (!z.links || b.lv_qlink[0]) && npx <= b.dnpx;
+}
+
+// Device bytes one frames-in-flight slot needs for a deferred frame of these params (0 when
+// the slot already holds enough).
+size_t defer_slot_bytes(const trt_ctx* c, const trt_params* p, uint32_t slot) {
+    const size_t npx = (size_t)trt_output_rows(p) * p->width;
+    const size_t ntiles = ((p->width + 7u) / 8u) * ((trt_output_rows(p) + 7u) / 8u);
+    const DeferSizes z = defer_sizes(c->defer_design, ntiles, p->max_depth, npx);
+    return defer_bufs_fit(c->split[slot], z, npx) ? 0 : z.bytes;
+}
+
+// The automatic frames-in-flight count of a deferred loop, bounded by device memory: each slot
+// holds its own scratch (defer_sizes: the shipped 1024x768 frame ~1 GB per slot in the pool
+// design, ~120 MB in TRT_DEFER_LEVELS), and the slots that would still need allocating may take
+// at most half of the free device memory.
+uint32_t fit_defer_slots(const trt_ctx* c, const trt_params* p, uint32_t want) {
+    size_t freeb = 0, total = 0;
+    if (hipMemGetInfo(&freeb, &total) != hipSuccess) return want;
+    size_t need = 0;
+    uint32_t n = 0;
+    for (; n < want && n < TRT_BUILD_MAX_IN_FLIGHT; ++n) {
+        need += defer_slot_bytes(c, p, n);
+        if (n > 0 && need > freeb / 2) break;
+    }
+    return std::max(1u, n);
+}
+
+void free_defer_bufs(trt_ctx::SplitBufs& b) {
+    void* ps[] = {b.ev, b.shq, b.px_ev, b.fb, b.lv_ev, b.lv_evr, b.lv_q[0], b.lv_q[1], b.lv_qlink[0], b.lv_qlink[1],
+                  b.lv_flag};
+    for (void* q : ps) (void)hipFree(q);
+    b.ev = nullptr;
+    b.shq = nullptr;
+    b.px_ev = nullptr;
+    b.fb = nullptr;
+    b.lv_ev = nullptr;
+    b.lv_evr = nullptr;
+    b.lv_q[0] = b.lv_q[1] = nullptr;
+    b.lv_qlink[0] = b.lv_qlink[1] = nullptr;
+    b.lv_flag = nullptr;
+    b.ev_chunks = b.shq_cap = b.dnpx = 0;
+    b.lv_evcap = b.lv_qcap = b.lv_npx = 0;
+}
+
+// Allocates slot `slot`'s deferred-frame scratch (the context's design) for this frame and fills
+// A's defer fields.
 int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     auto& b = c->split[slot];
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
-    const uint32_t D = p->max_depth;
-    // Event chunks: at depth <= 4 a pixel logs at most 2^D - 1 events (its whole tree), so
-    // ceil((2^D - 1) / kEvRows) chunks per tile never overflow; deeper frames get 4 chunks per
-    // tile on average, at least 128 per stripe (the shipped frame takes 1.3 per tile) (most tiles log one or two events per pixel; a lane that finds the pool
-    // empty is re-traced in place).  Slot ids (chunk * kEvRows + row) * 64 + lane travel in 30
-    // bits of a query.
-    const size_t per_tile = D <= 4 ? ((1u << D) - 1u + trt::kEvRows - 1u) / trt::kEvRows : 4u;
-    // Both are split into kDeferStripes equal stripes (tile t uses stripe hash(t)).
-    constexpr size_t S = trt::kDeferStripes;
-    const size_t tiles_per_stripe = (A.ntiles + S - 1) / S;
-    const size_t chunks = S * std::min<size_t>(std::max<size_t>(tiles_per_stripe * per_tile, D <= 4 ? 16u : 128u),
-                                               (1u << 30) / (trt::kEvRows * 64u) / S);
-    const size_t qcap = S * std::min<size_t>(std::max<size_t>(6 * tiles_per_stripe * 64u, 1u << 12),
-                                             0xFFFFFFFFu / S);
-    if (chunks > b.ev_chunks || qcap > b.shq_cap || npx > b.dnpx) {
-        (void)hipFree(b.ev);
-        (void)hipFree(b.shq);
-        (void)hipFree(b.px_ev);
-        (void)hipFree(b.fb);
-        b.ev = nullptr;
-        b.shq = nullptr;
-        b.px_ev = nullptr;
-        b.fb = nullptr;
-        b.ev_chunks = b.shq_cap = b.dnpx = 0;
-        hipError_t e = hipMalloc((void**)&b.ev, chunks * trt::kEvRows * 4 * 64 * sizeof(float4));
-        if (e == hipSuccess) e = hipMalloc((void**)&b.shq, qcap * 2 * sizeof(float4));
-        if (e == hipSuccess) e = hipMalloc((void**)&b.px_ev, npx * sizeof(uint2));
-        if (e == hipSuccess) e = hipMalloc((void**)&b.fb, npx * sizeof(uint32_t));
-        if (e == hipSuccess && !b.dctr) e = hipMalloc((void**)&b.dctr, sizeof(trt::DeferCtr));
-        if (e != hipSuccess) return hip_fail(c, e, "alloc deferred-shadow buffers");
-        b.ev_chunks = chunks;
-        b.shq_cap = qcap;
-        b.dnpx = npx;
+    const int design = c->defer_design;
+    const DeferSizes z = defer_sizes(design, A.ntiles, p->max_depth, npx);
+    if (!defer_bufs_fit(b, z, npx)) {
+        free_defer_bufs(b);
+        hipError_t e = hipSuccess;
+        auto alloc = [&](void** q, size_t bytes) {
+            if (e == hipSuccess && bytes) e = hipMalloc(q, bytes);
+        };
+        alloc((void**)&b.ev, z.chunks * kPoolEvBytes);
+        alloc((void**)&b.shq, z.qcap * 2 * sizeof(float4));
+        alloc((void**)&b.lv_ev, z.lv_evcap * sizeof(float4));
+        alloc((void**)&b.lv_evr, z.lv_evcap * sizeof(uint32_t));
+        for (int k = 0; k < 2; ++k) {
+            alloc((void**)&b.lv_q[k], z.lv_qcap * 2 * sizeof(float4));
+            if (z.links) alloc((void**)&b.lv_qlink[k], z.lv_qcap * sizeof(uint32_t));
+        }
+        alloc((void**)&b.px_ev, npx * sizeof(uint2));
+        alloc((void**)&b.lv_flag, npx * sizeof(uint32_t));
+        alloc((void**)&b.fb, npx * sizeof(uint32_t));
+        if (!b.dctr) alloc((void**)&b.dctr, sizeof(trt::DeferCtr));
+        if (!b.lv_ctr) alloc((void**)&b.lv_ctr, sizeof(trt::LevCtr));
+        if (e != hipSuccess) {
+            free_defer_bufs(b);
+            return hip_fail(c, e, "alloc deferred-frame buffers");
+        }
+        b.ev_chunks = z.chunks;
+        b.shq_cap = z.qcap;
+        b.lv_evcap = z.lv_evcap;
+        b.lv_qcap = z.lv_qcap;
+        b.dnpx = b.lv_npx = npx;
     }
+    b.last_levels = design == TRT_DEFER_LEVELS;
+    b.last_npx = npx;
     A.defer = 1;
+    A.lv = design == TRT_DEFER_LEVELS ? 1u : design == TRT_DEFER_LEVELS_B ? 2u : 0u;
+    A.lv_level = 0;
     // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
-    A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", b.ev_chunks / trt::kDeferStripes);
-    A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", b.shq_cap / trt::kDeferStripes);
+    A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", z.chunks / trt::kDeferStripes);
+    A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", z.qcap / trt::kDeferStripes);
     A.ev = b.ev;
     A.shq = b.shq;
     A.px_ev = b.px_ev;
     A.fb = b.fb;
     A.dctr = b.dctr;
+    const size_t lv_slots = design == TRT_DEFER_LEVELS ? z.lv_evcap : z.chunks * trt::kEvRows * 64u;
+    A.lv_evcap = (uint32_t)std::max<size_t>(env_cap("TRT_LV_EVCAP", lv_slots), npx);
+    A.lv_qcap = (uint32_t)env_cap("TRT_LV_QCAP", z.lv_qcap);
+    A.lv_ev = b.lv_ev;
+    A.lv_evr = b.lv_evr;
+    A.lv_q[0] = b.lv_q[0];
+    A.lv_q[1] = b.lv_q[1];
+    A.lv_qlink[0] = b.lv_qlink[0];
+    A.lv_qlink[1] = b.lv_qlink[1];
+    A.lv_ctr = b.lv_ctr;
+    A.lv_flag = b.lv_flag;
     return TRT_OK;
 }
 
@@ -748,11 +898,12 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     A.num_cus = c->num_cus;
     A.persist = c->d_persist + (size_t)slot * kPersistWords;
     A.defer = 0;
+    A.lv = 0;
     const bool defer = defer_frame(c, p);
     // A COUNT frame of a scene whose frames run deferred is traced unsplit, so its image is the
     // deferred frame's bit for bit (both are the reference's single running sum; a deferred
     // frame's subtree split keeps that order through LINK events).
-    if (defer || !defer_frame(c, p, true)) A.split_w = split_window(c, p);
+    if ((defer && c->defer_design == TRT_DEFER_POOL) || !defer_frame(c, p, true)) A.split_w = split_window(c, p);
     if (!A.split_w && !defer) return TRT_OK;
     auto& b = c->split[slot];
     if (b.last && b.last != stream) HIP_TRY(c, hipStreamWaitEvent(stream, b.done, 0));
@@ -815,13 +966,13 @@ int fence_split(trt_ctx* c, const KArgs& A, uint32_t slot, hipStream_t stream) {
     return TRT_OK;
 }
 
-// trt_render's split slot: one per distinct stream among the last TRT_MAX_FRAMES_IN_FLIGHT
+// trt_render's split slot: one per distinct stream among the last TRT_BUILD_MAX_IN_FLIGHT
 // (so renders alternating between streams overlap), reused least recently first.
 uint32_t render_slot(trt_ctx* c, hipStream_t s) {
-    for (uint32_t k = 0; k < TRT_MAX_FRAMES_IN_FLIGHT; ++k)
+    for (uint32_t k = 0; k < TRT_BUILD_MAX_IN_FLIGHT; ++k)
         if (c->render_slot_stream[k] == s) return k;
     const uint32_t k = c->render_slot_next;
-    c->render_slot_next = (k + 1) % TRT_MAX_FRAMES_IN_FLIGHT;
+    c->render_slot_next = (k + 1) % TRT_BUILD_MAX_IN_FLIGHT;
     c->render_slot_stream[k] = s;
     return k;
 }
@@ -857,7 +1008,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     // Plain frames (no subtree split, no deferred shadows: the same decision prepare_split
     // makes) go out several per launch; the others one per launch (per-slot scratch).
     const bool defer = defer_frame(c, p);
-    const bool split = (defer || !defer_frame(c, p, true)) && split_window(c, p) != 0;
+    const bool split = ((defer && c->defer_design == TRT_DEFER_POOL) || !defer_frame(c, p, true)) && split_window(c, p) != 0;
     const bool plain = !defer && !split;
     // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): launch j runs on slot j % n.  Slot 0
     // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
@@ -871,7 +1022,9 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     // 4: the shipped frame 0.42 -> 0.35 ms, the README scene 0.24 -> 0.17 ms,
     // profiles/r04z_ab_deferred_in_flight.jsonl; round 2: the shipped frame 1.45 -> 0.56 ms at
     // 8, profiles/r02_ab_queues_deep.log).
-    const uint32_t want = c->frames_in_flight ? c->frames_in_flight : plain ? 1u : defer ? c->defer_in_flight : 4u;
+    uint32_t want = c->frames_in_flight ? c->frames_in_flight : plain ? 1u : defer ? c->defer_in_flight : 4u;
+    // auto: no more deferred slots than device memory holds (each slot owns its scratch)
+    if (!c->frames_in_flight && defer) want = fit_defer_slots(c, p, want);
     const uint32_t cap = plain ? (c->frame_batch ? c->frame_batch : trt::kMaxLaunchFrames) : 1u;
     const uint32_t per_launch = std::max(1u, std::min(cap, (nframes + want - 1) / want));
     // launches: runs of consecutive frames sharing every UBO field but camPos
@@ -888,7 +1041,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
             c->fev.push_back(e);
         }
     }
-    const uint32_t nfl = std::min(want, nl);
+    uint32_t nfl = std::min(want, nl);
     std::vector<hipStream_t> sv{c->stream};
     // every slot's stream is made on first use of the in-flight count, not only the ones this
     // call needs: creating a stream takes milliseconds and must not land in a later, longer
@@ -916,9 +1069,17 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
         fill_ubo_args(A, c->ubo);
         A.nframes = n;
         for (uint32_t k = 0; k < n; ++k) fill_frame(A.fr[k], ubo_of(i0 + k), frames[i0 + k].out8, frames[i0 + k].in_place);
-        const uint32_t slot = j % nfl;
+        uint32_t slot = j % nfl;
+        if ((rc = prepare_split(c, p, A, slot, sv[slot])) != TRT_OK) {
+            // auto count: a slot whose scratch cannot be allocated is dropped, with the slots
+            // after it; the launch goes to a slot that has its scratch
+            if (c->frames_in_flight || slot == 0) return rc;
+            c->err.clear();
+            nfl = slot;
+            slot = j % nfl;
+            if ((rc = prepare_split(c, p, A, slot, sv[slot])) != TRT_OK) return rc;
+        }
         hipStream_t st = sv[slot];
-        if ((rc = prepare_split(c, p, A, slot, st)) != TRT_OK) return rc;
         const bool timed = timing && j % every == 0;
         const size_t k = 2 * (size_t)(j / every);
         if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], st));
@@ -1199,7 +1360,7 @@ int scene_adopt(trt_ctx* c, const SceneHeader& h) {
 // diagnostic: the first 16 words of slot `slot`'s deferred-frame counters (nfb + pad, where
 // defer_resolve records a log it could not finish)
 extern "C" int trt_diag_defer_pad(trt_ctx* c, uint32_t slot, uint32_t* out16) {
-    if (!c || !out16 || slot >= TRT_MAX_FRAMES_IN_FLIGHT || !c->split[slot].dctr) return TRT_ERR_INVALID;
+    if (!c || !out16 || slot >= TRT_BUILD_MAX_IN_FLIGHT || !c->split[slot].dctr) return TRT_ERR_INVALID;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(out16, c->split[slot].dctr, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return TRT_OK;
