@@ -35,6 +35,85 @@ def test_bvh4_compressed_layout(name, golden_meshes):
     else:
         sc = S.CONFIGS[name](64, 48, env_size=(64, 32))
     st = _build(sc)
-    assert st["tris"] == len(sc.tris)
+    assert st["tris"] >= len(sc.tris)  # leaf references: spatial splits duplicate some
     assert 0 < st["bvh4"] < st["bvh2"] and st["stack"] <= 64
     assert st["quantized"] == 1 and st["compressed"] == 1, st
+
+
+def _export(sc):
+    """The BVH2 trt_upload_scene builds (trt_diag_bvh_export): node records and the leaf
+    triangle references (triangle index per reference)."""
+    L = lib()
+    f = L.trt_diag_bvh_export
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                  ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    tris = np.ascontiguousarray(sc.tris, T.TRIANGLE)
+    models = np.ascontiguousarray(sc.models, T.MODEL)
+    cnt = (ctypes.c_uint64 * 2)()
+    assert f(tris.ctypes.data, len(tris), models.ctypes.data, len(models), None, 0, None, 0, cnt) == 0
+    nodes = np.zeros((cnt[0], 16), np.uint32)    # BvhNode: lo0 hi0 lo1 hi1 (12 floats), child[2], pad[2]
+    refs = np.zeros((cnt[1], 12), np.uint32)     # TriGeo: v0 e1 e2, pad = (triangle, batch, ni)
+    assert f(tris.ctypes.data, len(tris), models.ctypes.data, len(models), nodes.ctypes.data, cnt[0],
+             refs.ctypes.data, cnt[1], cnt) == 0
+    return nodes, refs
+
+
+@pytest.mark.parametrize("name", ["ref", "readme", "C3"])
+def test_every_triangle_point_is_inside_a_leaf_path(name, golden_meshes):
+    """Conservativeness of the build, spatial splits included (a triangle crossing a split plane
+    is referenced on both sides with its box clipped to each): for points of every triangle —
+    vertices, edge midpoints, centroid and random barycentric samples — some leaf referencing
+    that triangle has every box on its root path containing the point.  A ray hitting the
+    triangle at such a point therefore reaches a reference of it (the padding covers the
+    Moller-Trumbore rounding of where the hit lies)."""
+    if name == "ref":
+        sc = S.config_reference_default(golden_meshes, env_size=(64, 32))
+    elif name == "readme":
+        sc = S.config_readme(golden_meshes, env_size=(64, 32))
+    else:
+        sc = S.CONFIGS[name](64, 48, env_size=(64, 32))
+    nodes, refs = _export(sc)
+    boxes = nodes[:, :12].view(np.float32).reshape(-1, 4, 3)  # lo0, hi0, lo1, hi1
+    child = nodes[:, 12:14]
+    LEAF, CSHIFT, FMASK = 0x80000000, 27, (1 << 27) - 1
+    # effective box of each leaf reference: the intersection of the boxes on its root path
+    eff_lo = np.full((len(refs), 3), -np.inf, np.float64)
+    eff_hi = np.full((len(refs), 3), np.inf, np.float64)
+    stack = [(0, np.full(3, -np.inf), np.full(3, np.inf))]
+    while stack:
+        n, lo, hi = stack.pop()
+        for k in range(2):
+            c = int(child[n, k])
+            if c == 0xFFFFFFFF:
+                continue
+            clo = np.maximum(lo, boxes[n, 2 * k].astype(np.float64))
+            chi = np.minimum(hi, boxes[n, 2 * k + 1].astype(np.float64))
+            if c & LEAF:
+                first, cnt = c & FMASK, ((c >> CSHIFT) & 15) + 1
+                eff_lo[first:first + cnt] = clo
+                eff_hi[first:first + cnt] = chi
+            else:
+                stack.append((c, clo, chi))
+    tri_of = refs[:, 9].astype(np.int64)
+    assert np.isin(np.arange(len(sc.tris)), tri_of).all()  # every triangle is referenced
+    rng = np.random.default_rng(5)
+    v = np.stack([np.stack([sc.tris[k][:, i] for i in range(3)], 1) for k in ("v0", "v1", "v2")], 1).astype(np.float64)
+    bary = [np.eye(3), np.array([[0.5, 0.5, 0], [0, 0.5, 0.5], [0.5, 0, 0.5], [1 / 3, 1 / 3, 1 / 3]])]
+    r = rng.random((4, 2))
+    r = np.where(r.sum(1, keepdims=True) > 1, 1 - r, r)
+    bary.append(np.stack([1 - r.sum(1), r[:, 0], r[:, 1]], 1))
+    bary = np.concatenate(bary)
+    pts = np.einsum("sk,tkc->tsc", bary, v)  # (tris, samples, 3)
+    covered = np.zeros(pts.shape[:2], bool)
+    order = np.argsort(tri_of, kind="stable")
+    t_sorted = tri_of[order]
+    starts = np.searchsorted(t_sorted, np.arange(len(sc.tris)))
+    ends = np.searchsorted(t_sorted, np.arange(len(sc.tris)), side="right")
+    maxrefs = int((ends - starts).max())
+    for j in range(maxrefs):  # j-th reference of every triangle that has one
+        has = ends - starts > j
+        ri = order[np.minimum(starts + j, len(order) - 1)]
+        inside = ((pts >= eff_lo[ri][:, None, :]) & (pts <= eff_hi[ri][:, None, :])).all(-1)
+        covered |= inside & has[:, None]
+    assert covered.all(), f"{int((~covered).sum())} triangle points outside every leaf path of their triangle"

@@ -388,11 +388,12 @@ def test_multi_frame_launches_match_single_frames(gpu_renderer, config, sphere_e
 
 
 @pytest.mark.parametrize("rot,skew,inter,pair", [(1, 0, 0, 1), (2, 3, 0, 1), (0, 5, 0, 1), (4, 1, 0, 1), (0, 0, 1, 1),
-                                                (1, 3, 1, 1), (1, 0, 1, 2), (0, 3, 1, 2)])
+                                                (1, 3, 1, 1), (1, 0, 1, 2), (0, 3, 1, 2), (1, 0, 2, 2), (0, 3, 2, 1)])
 @pytest.mark.parametrize("size", [(264, 200), (256, 128), (88, 56)])
 def test_xcd_dealing_knobs_match_single_frames(rot, skew, inter, pair, size):
     """TRT_XCD_ROT / TRT_XCD_SKEW / TRT_XCD_INTER re-deal a multi-frame launch's tiles to the
-    XCDs (rotated chunk classes per frame, diagonal classes, frames interleaved per chunk group)
+    XCDs (rotated chunk classes per frame, diagonal classes, frames interleaved per chunk group;
+    INTER=2: no rotation, chunk classes permuted by a coprime multiplier)
     and TRT_FRAME_GROUP=2 has a workgroup trace its tile in two consecutive frames (9 frames: the
     last pair is one frame): a bijection, so every frame still equals
     trt_render bit for bit — image sizes with leftover chunks, an odd tile column and row

@@ -26,6 +26,11 @@ variant() { # name extra-flags...
 for v in "$@"; do
     case $v in
         base) variant base ;;
+        oldsize) variant oldsize -DTRT_LIGHT_UNROLL=1 -DTRT_MESH_PAIRS=1 ;;
+        sh4) variant sh4 -DTRT_G3_WAVES_SHALLOW=4 ;;
+        pk0) variant pk0 -DTRT_SPHERE_PK=0 ;;
+        lds24) variant lds24 -DTRT_G3_LDS=24 ;;
+        lds32) variant lds32 -DTRT_G3_LDS=32 ;;
         cur) variant cur ;;
         g3p24) variant g3p24 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=24 ;;
         g3p32) variant g3p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 ;;

@@ -63,7 +63,14 @@ struct Prim {
 struct SahParams {
     float ct = 0.0f;
     uint32_t leaf_min = kBvhLeafMin, leaf_max = kBvhLeafMax;
+    // Binned SAH over every axis with 32 bins (round 5; TRT_BVH_AXES=1 / TRT_BVH_BINS=16 give the
+    // widest-centroid-axis, 16-bin build of rounds 1-4): C4 -0.8 %, C3 -1 %, the shipped frame and
+    // the README scene -5 % (profiles/r05g_ab_codesize_bvh.jsonl)
+    int all_axes = 1;
+    int bins = 32;
     SahParams() {
+        if (const char* e = std::getenv("TRT_BVH_AXES")) all_axes = std::atoi(e) == 3;
+        if (const char* e = std::getenv("TRT_BVH_BINS")) bins = std::min(64, std::max(4, std::atoi(e)));
         if (const char* e = std::getenv("TRT_BVH_CT")) ct = std::strtof(e, nullptr);
         if (const char* e = std::getenv("TRT_BVH_LEAF_MIN")) leaf_min = (uint32_t)std::strtoul(e, nullptr, 10);
         if (const char* e = std::getenv("TRT_BVH_LEAF_MAX")) leaf_max = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -92,7 +99,7 @@ struct Builder {
         const uint32_t n = e - b;
         if (n <= sp.leaf_min) return make_leaf(b, e);
         const bool median_only = depth >= kBvhSahDepth; // bounds the depth: <= 32 + log2(n) levels
-        // binned SAH over the widest centroid axis
+        // binned SAH over the widest centroid axis (or every axis, all_axes)
         int axis = 0;
         float ext = cb.hi[0] - cb.lo[0];
         for (int k = 1; k < 3; ++k)
@@ -102,49 +109,62 @@ struct Builder {
             }
         uint32_t mid = b + n / 2;
         if (ext > 0.0f && !median_only) {
-            constexpr int NB = 16;
-            Box bins[NB];
-            uint32_t cnt[NB] = {0};
-            for (auto& x : bins) x.reset();
-            const float scale = NB / ext;
-            auto bin_of = [&](const Prim& p) {
-                int k = (int)((p.c[axis] - cb.lo[axis]) * scale);
-                return std::min(NB - 1, std::max(0, k));
-            };
-            for (uint32_t i = b; i < e; ++i) {
-                int k = bin_of(prims[i]);
-                bins[k].grow(prims[i].box);
-                cnt[k]++;
-            }
+            constexpr int MAXB = 64;
+            const int NB = sp.bins;
             float best = std::numeric_limits<float>::infinity();
-            int best_k = -1;
-            Box left;
-            left.reset();
-            uint32_t nl = 0;
-            for (int k = 0; k < NB - 1; ++k) {
-                left.grow(bins[k]);
-                nl += cnt[k];
-                Box right;
-                right.reset();
-                uint32_t nr = 0;
-                for (int m = k + 1; m < NB; ++m) {
-                    right.grow(bins[m]);
-                    nr += cnt[m];
+            int best_k = -1, best_axis = axis;
+            for (int a = 0; a < 3; ++a) {
+                if (!sp.all_axes && a != axis) continue;
+                const float ea = cb.hi[a] - cb.lo[a];
+                if (!(ea > 0.0f)) continue;
+                Box bins[MAXB];
+                uint32_t cnt[MAXB] = {0};
+                for (int k = 0; k < NB; ++k) bins[k].reset();
+                const float scale = NB / ea;
+                for (uint32_t i = b; i < e; ++i) {
+                    int k = std::min(NB - 1, std::max(0, (int)((prims[i].c[a] - cb.lo[a]) * scale)));
+                    bins[k].grow(prims[i].box);
+                    cnt[k]++;
                 }
-                if (!nl || !nr) continue;
-                const float cost = sp.ct * bb.area() + left.area() * nl + right.area() * nr;
-                if (cost < best) {
-                    best = cost;
-                    best_k = k;
+                // right-hand sweeps once, then the left-to-right scan
+                Box rsum[MAXB];
+                uint32_t rcnt[MAXB];
+                Box acc;
+                acc.reset();
+                uint32_t ac = 0;
+                for (int k = NB - 1; k >= 0; --k) {
+                    acc.grow(bins[k]);
+                    ac += cnt[k];
+                    rsum[k] = acc;
+                    rcnt[k] = ac;
+                }
+                Box left;
+                left.reset();
+                uint32_t nl = 0;
+                for (int k = 0; k < NB - 1; ++k) {
+                    left.grow(bins[k]);
+                    nl += cnt[k];
+                    const uint32_t nr = rcnt[k + 1];
+                    if (!nl || !nr) continue;
+                    const float cost = sp.ct * bb.area() + left.area() * nl + rsum[k + 1].area() * nr;
+                    if (cost < best) {
+                        best = cost;
+                        best_k = k;
+                        best_axis = a;
+                    }
                 }
             }
             const float leaf_cost = bb.area() * n;
             if (n <= sp.leaf_max && !(best < leaf_cost)) return make_leaf(b, e);
             if (best_k >= 0) {
-                auto it = std::partition(prims.begin() + b, prims.begin() + e,
-                                         [&](const Prim& p) { return bin_of(p) <= best_k; });
+                const int a = best_axis;
+                const float scale = NB / (cb.hi[a] - cb.lo[a]);
+                auto it = std::partition(prims.begin() + b, prims.begin() + e, [&](const Prim& p) {
+                    return std::min(NB - 1, std::max(0, (int)((p.c[a] - cb.lo[a]) * scale))) <= best_k;
+                });
                 mid = (uint32_t)(it - prims.begin());
                 if (mid == b || mid == e) mid = b + n / 2;
+                else axis = a;
             }
         }
         if (mid == b + n / 2) {
@@ -172,6 +192,286 @@ struct Builder {
         const uint32_t start = (uint32_t)order.size();
         for (uint32_t i = b; i < e; ++i) order.push_back(i);
         return kBvhLeafBit | ((e - b - 1u) << kBvhCountShift) | start;
+    }
+};
+
+// ---- spatial splits (Stich, Friedrich, Dietrich, "Spatial Splits in Bounding Volume
+// Hierarchies", HPG 2009) ------------------------------------------------------------------
+//
+// A node may also split SPACE: a plane through the node's box, every triangle reference left or
+// right of it, and a triangle crossing it referenced on both sides with its box clipped to each
+// side.  Long thin triangles (the lathed glass of the shipped scene) otherwise give overlapping
+// sibling boxes that incoherent rays inside the glass must all enter.  A reference is still the
+// whole triangle (the kernel tests the triangle, not its clipped part), only the node boxes are
+// tighter; a clipped box contains the triangle's part on its side of the plane (clipped in double,
+// then padded like tri_box), so a ray hitting the triangle enters a box holding a reference to it.
+// Duplicate references of one triangle return the same t and (batch, triangle), so the kernel's
+// tie-break keeps one.
+struct V3d {
+    double x[3];
+};
+
+// Bounding box of the part of triangle t inside the slab lo <= x[a] <= hi (empty: lo > hi).
+Box clip_box(const trt_triangle& t, int a, double lo, double hi) {
+    V3d poly[9], tmp[9];
+    int n = 3;
+    const trt_vec4* v[3] = {&t.v0, &t.v1, &t.v2};
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) poly[i].x[k] = (&v[i]->x)[k];
+    auto clip = [&](double plane, bool keep_ge) {
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const V3d& p = poly[i];
+            const V3d& q = poly[(i + 1) % n];
+            const bool pin = keep_ge ? p.x[a] >= plane : p.x[a] <= plane;
+            const bool qin = keep_ge ? q.x[a] >= plane : q.x[a] <= plane;
+            if (pin) tmp[m++] = p;
+            if (pin != qin) {
+                const double s = (plane - p.x[a]) / (q.x[a] - p.x[a]);
+                V3d r;
+                for (int k = 0; k < 3; ++k) r.x[k] = p.x[k] + s * (q.x[k] - p.x[k]);
+                r.x[a] = plane;
+                tmp[m++] = r;
+            }
+        }
+        n = m;
+        for (int i = 0; i < n; ++i) poly[i] = tmp[i];
+    };
+    clip(lo, true);
+    if (n) clip(hi, false);
+    Box b;
+    b.reset();
+    if (!n) return b;
+    // outward rounding to float plus tri_box's padding of the whole triangle
+    float tlo[3], thi[3];
+    for (int k = 0; k < 3; ++k) {
+        const float c0 = (&t.v0.x)[k], c1 = (&t.v1.x)[k], c2 = (&t.v2.x)[k];
+        tlo[k] = std::min({c0, c1, c2});
+        thi[k] = std::max({c0, c1, c2});
+        double l = poly[0].x[k], h = poly[0].x[k];
+        for (int i = 1; i < n; ++i) {
+            l = std::min(l, poly[i].x[k]);
+            h = std::max(h, poly[i].x[k]);
+        }
+        const float pad = std::max({1e-4f * (thi[k] - tlo[k]), 1e-5f * std::max(std::fabs(tlo[k]), std::fabs(thi[k])), 1e-6f});
+        float lf = (float)l, hf = (float)h;
+        if ((double)lf > l) lf = std::nextafter(lf, -std::numeric_limits<float>::infinity());
+        if ((double)hf < h) hf = std::nextafter(hf, std::numeric_limits<float>::infinity());
+        b.lo[k] = lf - pad;
+        b.hi[k] = hf + pad;
+    }
+    return b;
+}
+
+Box intersect(const Box& a, const Box& b) {
+    Box r;
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = std::max(a.lo[k], b.lo[k]);
+        r.hi[k] = std::min(a.hi[k], b.hi[k]);
+    }
+    return r;
+}
+bool empty_box(const Box& b) { return !(b.lo[0] <= b.hi[0] && b.lo[1] <= b.hi[1] && b.lo[2] <= b.hi[2]); }
+
+struct SplitBuilder {
+    SahParams sp;
+    const trt_triangle* tris = nullptr;
+    std::vector<BvhNode> nodes;
+    std::vector<Prim> leaf_refs;
+    float alpha = 1e-5f;     // spatial splits are tried when the object split's child overlap
+    float root_area = 0.0f;  // exceeds alpha x the root's area (Stich et al.)
+    size_t budget = 0;       // reference duplicates allowed in all (bounds the memory)
+
+    uint32_t make_leaf(const std::vector<Prim>& refs) {
+        const uint32_t start = (uint32_t)leaf_refs.size();
+        leaf_refs.insert(leaf_refs.end(), refs.begin(), refs.end());
+        return kBvhLeafBit | ((uint32_t)(refs.size() - 1u) << kBvhCountShift) | start;
+    }
+
+    uint32_t build(std::vector<Prim>& refs, Box& out_box, int depth) {
+        Box bb, cb;
+        bb.reset();
+        cb.reset();
+        for (const Prim& p : refs) {
+            bb.grow(p.box);
+            Box c{{p.c[0], p.c[1], p.c[2]}, {p.c[0], p.c[1], p.c[2]}};
+            cb.grow(c);
+        }
+        out_box = bb;
+        const uint32_t n = (uint32_t)refs.size();
+        if (n <= sp.leaf_min) return make_leaf(refs);
+        constexpr int NB = 32;
+        // -- object split: binned SAH over every centroid axis --
+        float best = std::numeric_limits<float>::infinity();
+        int best_axis = -1, best_k = -1;
+        Box best_l, best_r;
+        for (int a = 0; a < 3; ++a) {
+            const float ea = cb.hi[a] - cb.lo[a];
+            if (!(ea > 0.0f)) continue;
+            Box bins[NB];
+            uint32_t cnt[NB] = {0};
+            for (auto& x : bins) x.reset();
+            const float scale = NB / ea;
+            for (const Prim& p : refs) {
+                const int k = std::min(NB - 1, std::max(0, (int)((p.c[a] - cb.lo[a]) * scale)));
+                bins[k].grow(p.box);
+                cnt[k]++;
+            }
+            Box rsum[NB];
+            uint32_t rcnt[NB];
+            Box acc;
+            acc.reset();
+            uint32_t ac = 0;
+            for (int k = NB - 1; k >= 0; --k) {
+                acc.grow(bins[k]);
+                ac += cnt[k];
+                rsum[k] = acc;
+                rcnt[k] = ac;
+            }
+            Box left;
+            left.reset();
+            uint32_t nl = 0;
+            for (int k = 0; k < NB - 1; ++k) {
+                left.grow(bins[k]);
+                nl += cnt[k];
+                const uint32_t nr = rcnt[k + 1];
+                if (!nl || !nr) continue;
+                const float cost = left.area() * nl + rsum[k + 1].area() * nr;
+                if (cost < best) {
+                    best = cost;
+                    best_axis = a;
+                    best_k = k;
+                    best_l = left;
+                    best_r = rsum[k + 1];
+                }
+            }
+        }
+        // -- spatial split: chopped binning over every axis of the node box --
+        float sbest = std::numeric_limits<float>::infinity();
+        int s_axis = -1;
+        double s_plane = 0.0;
+        bool try_spatial = depth < kBvhSahDepth && budget > 0;
+        if (try_spatial && best_axis >= 0) {
+            const Box ov = intersect(best_l, best_r);
+            try_spatial = !empty_box(ov) && ov.area() > alpha * root_area;
+        }
+        if (try_spatial) {
+            for (int a = 0; a < 3; ++a) {
+                const double lo = bb.lo[a], ext = (double)bb.hi[a] - lo;
+                if (!(ext > 0.0)) continue;
+                Box bins[NB];
+                uint32_t enter[NB] = {0}, exitc[NB] = {0};
+                for (auto& x : bins) x.reset();
+                auto bin_of = [&](double v) { return std::min(NB - 1, std::max(0, (int)((v - lo) / ext * NB))); };
+                for (const Prim& p : refs) {
+                    const int b0 = bin_of(p.box.lo[a]), b1 = bin_of(p.box.hi[a]);
+                    enter[b0]++;
+                    exitc[b1]++;
+                    for (int k = b0; k <= b1; ++k) {
+                        const double pl = lo + ext * k / NB, ph = lo + ext * (k + 1) / NB;
+                        Box cbx = b0 == b1 ? p.box : intersect(clip_box(tris[p.tri], a, pl, ph), p.box);
+                        if (!empty_box(cbx)) bins[k].grow(cbx);
+                    }
+                }
+                Box rsum[NB];
+                uint32_t rcnt[NB];
+                Box acc;
+                acc.reset();
+                uint32_t ac = 0;
+                for (int k = NB - 1; k >= 0; --k) {
+                    acc.grow(bins[k]);
+                    ac += exitc[k];
+                    rsum[k] = acc;
+                    rcnt[k] = ac;
+                }
+                Box left;
+                left.reset();
+                uint32_t nl = 0;
+                for (int k = 0; k < NB - 1; ++k) {
+                    left.grow(bins[k]);
+                    nl += enter[k];
+                    const uint32_t nr = rcnt[k + 1];
+                    if (!nl || !nr) continue;
+                    const float cost = left.area() * nl + rsum[k + 1].area() * nr;
+                    if (cost < sbest) {
+                        sbest = cost;
+                        s_axis = a;
+                        s_plane = lo + ext * (k + 1) / NB;
+                    }
+                }
+            }
+        }
+        const float leaf_cost = bb.area() * n;
+        const float split_cost = std::min(best, sbest);
+        if (n <= sp.leaf_max && !(split_cost < leaf_cost)) return make_leaf(refs);
+        std::vector<Prim> L, R;
+        if (sbest < best && s_axis >= 0) {
+            const int a = s_axis;
+            for (const Prim& p : refs) {
+                if ((double)p.box.hi[a] <= s_plane) {
+                    L.push_back(p);
+                } else if ((double)p.box.lo[a] >= s_plane) {
+                    R.push_back(p);
+                } else { // straddles: clipped to each side
+                    Prim pl = p, pr = p;
+                    pl.box = intersect(clip_box(tris[p.tri], a, -std::numeric_limits<double>::infinity(), s_plane), p.box);
+                    pr.box = intersect(clip_box(tris[p.tri], a, s_plane, std::numeric_limits<double>::infinity()), p.box);
+                    const bool el = empty_box(pl.box), er = empty_box(pr.box);
+                    if (el && er) {
+                        L.push_back(p);
+                        continue;
+                    }
+                    for (Prim* q : {&pl, &pr})
+                        for (int k = 0; k < 3; ++k) q->c[k] = 0.5f * (q->box.lo[k] + q->box.hi[k]);
+                    if (!el) L.push_back(pl);
+                    if (!er) R.push_back(pr);
+                    if (!el && !er && budget) --budget;
+                }
+            }
+            if (L.empty() || R.empty()) { // degenerate: fall back to the object split
+                L.clear();
+                R.clear();
+                sbest = std::numeric_limits<float>::infinity();
+            }
+        }
+        if (L.empty() && R.empty()) {
+            if (best_axis >= 0) {
+                const int a = best_axis;
+                const float scale = NB / (cb.hi[a] - cb.lo[a]);
+                for (const Prim& p : refs)
+                    (std::min(NB - 1, std::max(0, (int)((p.c[a] - cb.lo[a]) * scale))) <= best_k ? L : R).push_back(p);
+            }
+            if (L.empty() || R.empty()) { // median on the widest centroid axis
+                L.clear();
+                R.clear();
+                int a = 0;
+                for (int k = 1; k < 3; ++k)
+                    if (cb.hi[k] - cb.lo[k] > cb.hi[a] - cb.lo[a]) a = k;
+                std::vector<Prim> v = refs;
+                const size_t mid = v.size() / 2;
+                std::nth_element(v.begin(), v.begin() + mid, v.end(),
+                                 [&](const Prim& x, const Prim& y) { return x.c[a] < y.c[a]; });
+                L.assign(v.begin(), v.begin() + mid);
+                R.assign(v.begin() + mid, v.end());
+            }
+        }
+        refs.clear();
+        refs.shrink_to_fit();
+        const uint32_t idx = (uint32_t)nodes.size();
+        nodes.emplace_back();
+        Box lb, rb;
+        const uint32_t l = build(L, lb, depth + 1);
+        const uint32_t r = build(R, rb, depth + 1);
+        BvhNode& nd = nodes[idx];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo0[k] = lb.lo[k];
+            nd.hi0[k] = lb.hi[k];
+            nd.lo1[k] = rb.lo[k];
+            nd.hi1[k] = rb.hi[k];
+        }
+        nd.child[0] = l;
+        nd.child[1] = r;
+        return idx;
     }
 };
 
@@ -207,6 +507,11 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
             owner[j] = (int32_t)i;
         }
     }
+    // Spatial splits (SplitBuilder, up to 30 % more references; TRT_BVH_SPLITS=0 turns them off):
+    // the shipped frame -7 %, the README scene -9.5 %, C3 / C4 unchanged (their uniform
+    // icosphere triangles take no spatial split), profiles/r05g_ab_codesize_bvh.jsonl
+    const char* sps = std::getenv("TRT_BVH_SPLITS");
+    const bool spatial = !sps || std::atoi(sps) != 0;
     Builder B;
     for (uint32_t j = 0; j < ntri; ++j) {
         if (owner[j] < 0) continue; // never tested by the reference
@@ -222,9 +527,27 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
         B.prims.push_back(p);
     }
     if (B.prims.empty()) return false;
-    B.nodes.reserve(2 * B.prims.size() / B.sp.leaf_min + 2);
     Box root;
-    const uint32_t r = B.build(0, (uint32_t)B.prims.size(), root, 0);
+    uint32_t r;
+    std::vector<Prim> refs_out;
+    if (spatial) {
+        SplitBuilder S;
+        S.tris = tris;
+        Box all;
+        all.reset();
+        for (const Prim& p : B.prims) all.grow(p.box);
+        S.root_area = all.area();
+        S.budget = B.prims.size() * 3 / 10;
+        std::vector<Prim> refs = B.prims;
+        r = S.build(refs, root, 0);
+        B.nodes.swap(S.nodes);
+        refs_out.swap(S.leaf_refs);
+    } else {
+        B.nodes.reserve(2 * B.prims.size() / B.sp.leaf_min + 2);
+        r = B.build(0, (uint32_t)B.prims.size(), root, 0);
+        refs_out.reserve(B.order.size());
+        for (uint32_t k : B.order) refs_out.push_back(B.prims[k]);
+    }
     if (r & kBvhLeafBit) { // single leaf: wrap it in a node with an empty second child
         BvhNode nd;
         for (int k = 0; k < 3; ++k) {
@@ -241,9 +564,9 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
         B.nodes.insert(B.nodes.begin(), nd);
     }
     nodes.swap(B.nodes);
-    leaf_tris.resize(B.order.size());
-    for (size_t k = 0; k < B.order.size(); ++k) {
-        const Prim& p = B.prims[B.order[k]];
+    leaf_tris.resize(refs_out.size());
+    for (size_t k = 0; k < refs_out.size(); ++k) {
+        const Prim& p = refs_out[k];
         const trt_triangle& t = tris[p.tri];
         TriGeo& g = leaf_tris[k];
         g.v0[0] = t.v0.x;

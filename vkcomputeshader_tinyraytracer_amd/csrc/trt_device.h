@@ -269,7 +269,8 @@ struct KArgs {
     uint32_t ntiles;              // 8x8 tiles in the launch
     uint32_t bvh_waves4;          // BVH walk: the 4-waves-per-SIMD build (GEOM 3)
     uint32_t xcd_rot, xcd_skew;   // multi-frame tile dealing (xcd_tile): rotation period, row skew
-    uint32_t xcd_inter;           // ... frames interleaved per chunk group (inter_tile)
+    uint32_t xcd_inter;           // ... frames interleaved per chunk group (inter_tile); 2: no rotation, permuted classes
+    uint32_t xcd_mult;            // ... xcd_inter 2: chunk permutation multiplier (coprime to the dealt chunks)
     uint32_t frame_group;         // ... 2: each workgroup traces its tile in two consecutive frames
     // subtree split: this launch traces depths < split_d1; children at depth split_d1 become
     // tasks (split_d1 >= max_depth: no split).  split_w: the window (0 = split off).

@@ -151,6 +151,34 @@ __device__ __forceinline__ bool sphere_hit(f3 o, f3 d, const SphereArg& s, float
     return true;
 }
 
+// Two spheres' ray_sphere_intersect prologue in packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two
+// IEEE operations per instruction, each rounded as its scalar form, no contraction): L = c - o,
+// tca = dot(L, d), d2 = dot(L, L) - tca * tca in sphere_hit's operand order, so every element is
+// sphere_hit's value bit for bit.  Half the VALU instructions of the four sphere tests of every
+// query (C2: ~2.9 queries per pixel).
+#ifndef TRT_SPHERE_PK
+#define TRT_SPHERE_PK 1 /* bit 0: scene_intersect, bit 1: shadow_intersect (spills the C2 kernel: 60 B) */
+#endif
+typedef float pk2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void sphere_pair_pre(f3 o, f3 d, const SphereArg& s0, const SphereArg& s1, pk2& tca, pk2& d2) {
+    const pk2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const pk2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+    const pk2 Lx = pk2{s0.c[0], s1.c[0]} - ox, Ly = pk2{s0.c[1], s1.c[1]} - oy, Lz = pk2{s0.c[2], s1.c[2]} - oz;
+    tca = (Lx * dx + Ly * dy) + Lz * dz;
+    d2 = ((Lx * Lx + Ly * Ly) + Lz * Lz) - tca * tca;
+}
+// sphere_hit's remainder from its prologue's tca and d2
+__device__ __forceinline__ bool sphere_hit_post(const SphereArg& s, float tca, float d2, float& t) {
+    float r2 = s.r * s.r;
+    if (d2 > r2) return false;
+    float thc = sqrt_rn(r2 - d2);
+    float t0 = tca - thc, t1 = tca + thc;
+    if (t0 > TRT_EPS) t = t0;
+    else if (t1 > TRT_EPS) t = t1;
+    else return false;
+    return true;
+}
+
 // custom_refract, shader.comp:209-221, called with eta_in = air (1.0)
 __device__ __forceinline__ f3 custom_refract(f3 I, f3 N, float eta_out, float eta_in) {
     bool entering = dot3(I, N) < 0.0f;
@@ -1211,11 +1239,20 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
         }
     }
     if (A.flags & TRT_FLAG_SPHERES) { // shader.comp:322-335
+#if TRT_SPHERE_PK & 1
+        pk2 tca, d2;
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = 1e10f;
             if (COUNT) ++c.sph;
-            if (sphere_hit(o, d, A.sph[i], t) && t < h.t) {
+#if TRT_SPHERE_PK & 1
+            if ((i & 1) == 0) sphere_pair_pre(o, d, A.sph[i], A.sph[i + 1], tca, d2);
+            const bool hit = sphere_hit_post(A.sph[i], tca[i & 1], d2[i & 1], t);
+#else
+            const bool hit = sphere_hit(o, d, A.sph[i], t);
+#endif
+            if (hit && t < h.t) {
                 h.t = t;
                 h.kind = HIT_SPHERE;
                 h.idx = i;
@@ -1254,11 +1291,19 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
     }
 #endif
     if (A.flags & TRT_FLAG_SPHERES) {
+#if TRT_SPHERE_PK & 2
+        pk2 tca, d2;
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = 1e10f;
             if (COUNT) ++c.sph;
+#if TRT_SPHERE_PK & 2
+            if ((i & 1) == 0) sphere_pair_pre(o, d, A.sph[i], A.sph[i + 1], tca, d2);
+            if (sphere_hit_post(A.sph[i], tca[i & 1], d2[i & 1], t) && t < max_dist) return true;
+#else
             if (sphere_hit(o, d, A.sph[i], t) && t < max_dist) return true;
+#endif
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return false;
@@ -1843,7 +1888,15 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 if constexpr (PARK) return P[k * 64];
                 else return x;
             };
-#pragma unroll
+            // Mesh kernels (GEOM >= 2) keep the light loop rolled: unrolled, each of the three
+            // lights inlines its own copy of the shadow walks (the wave-coherent one and the
+            // per-lane BVH walk), which multiplied the kernel's code past the instruction cache
+            // (TRT_LIGHT_UNROLL=1 restores it).
+#ifndef TRT_LIGHT_UNROLL
+#define TRT_LIGHT_UNROLL 0
+#endif
+            constexpr int kLightUnroll = GEOM >= 2 && !TRT_LIGHT_UNROLL ? 1 : 3;
+#pragma unroll kLightUnroll
             for (int i = 0; i < 3; ++i) {
                 if constexpr (PARK) park_fence();
                 const float sexp_i = park_f(14, sexp), alb0_i = park_f(15, alb[0]);
@@ -2503,7 +2556,10 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
 // every tile is traced once; they only move work between XCDs.  Why: the hardware deals blocks
 // to the XCDs round-robin, statically, so an XCD whose chunk class is costlier (the glass
 // spheres' stripes) finishes its share of a launch later than the others.
-__device__ __forceinline__ uint32_t xcd_deal(const KArgs& A, uint32_t b, uint32_t roff) {
+// perm (xcd_inter 2): chunk k of the evenly dealt ones is chunk (k * xcd_mult) mod nfull, a
+// bijection (xcd_mult is coprime to nfull) that makes each XCD's chunks a 2-D lattice spread over
+// the whole image instead of every 8th chunk column.
+__device__ __forceinline__ uint32_t xcd_deal(const KArgs& A, uint32_t b, uint32_t roff, bool perm = false) {
     const uint32_t tyn = A.ntiles / A.ntx;
     const uint32_t cw = A.ntx / 2u, ch = tyn / 2u;                 // whole 2x2 chunks
     const uint32_t nchunk = cw * ch, nfull = (nchunk / 8u) * 8u;   // dealt evenly to the XCDs
@@ -2517,7 +2573,9 @@ __device__ __forceinline__ uint32_t xcd_deal(const KArgs& A, uint32_t b, uint32_
         const uint32_t j = b / 8u; // j-th block of XCD x
         uint32_t x = b % 8u;
         x = (x + roff) & 7u;
-        return chunk_tile((j / 4u) * 8u + x, j % 4u);
+        uint32_t k = (j / 4u) * 8u + x;
+        if (perm) k = (k * A.xcd_mult) % nfull; // fits 32 bits: the host keeps xcd_mult 1 for >= 65536 chunks
+        return chunk_tile(k, j % 4u);
     }
     // leftovers: the last nchunk % 8 chunks, then the odd right column, then the odd bottom row
     uint32_t r = b - nfull * 4u;
@@ -2547,6 +2605,10 @@ __device__ __forceinline__ uint32_t xcd_tile_base(const KArgs& A, uint32_t b) { 
 // frame's whole tile order (whose costliest tiles then start near the end).  Sets f; tiles
 // outside whole chunk groups (leftovers) are dealt frame by frame after them.
 // F: the launch's frames (or frame pairs, frame_pair).
+// xcd_inter 2: no rotation — chunk group g's chunk on XCD x is the same in every frame of the
+// launch, so that XCD traces that chunk in all frames back to back and the texels its primary
+// rays miss into (the same directions in every frame: the camera only translates) stay in its L2;
+// the permuted classes (xcd_deal perm) keep the XCDs balanced without the rotation.
 __device__ __forceinline__ uint32_t inter_tile(const KArgs& A, uint32_t vb, uint32_t& f, uint32_t F) {
     const uint32_t tyn = A.ntiles / A.ntx;
     const uint32_t nchunk = (A.ntx / 2u) * (tyn / 2u), nfull = (nchunk / 8u) * 8u;
@@ -2556,8 +2618,9 @@ __device__ __forceinline__ uint32_t inter_tile(const KArgs& A, uint32_t vb, uint
         f = q % F;
         const uint32_t g = q / F; // chunk group: chunks g * 8 .. g * 8 + 7
         // block (g * 8 + ((x + f) & 7)) * 4 + i % 4 of frame f, in xcd_tile's unrotated dealing
-        const uint32_t c = (x + f) & 7u;
-        return xcd_tile_base(A, (g * 4u + i % 4u) * 8u + c);
+        const bool fixed = A.xcd_inter == 2u;
+        const uint32_t c = fixed ? x : (x + f) & 7u;
+        return xcd_deal(A, (g * 4u + i % 4u) * 8u + c, 0u, fixed);
     }
     const uint32_t r = vb - F * per, nl = A.ntiles - per;
     f = r / nl;
@@ -2573,6 +2636,11 @@ __device__ __forceinline__ uint32_t inter_tile(const KArgs& A, uint32_t vb, uint
 // out, 4 waves per SIMD); 1 = the reference-order batch walk; 2 = per-lane BVH.
 #ifndef TRT_WAVES
 #define TRT_WAVES 1
+#endif
+// Frame pairs (TRT_FRAME_GROUP=2) for mesh frames: compiled only on request (measured slower
+// for meshes: C4 +2.5 %, C3 +10 %, profiles/r03_ab_frame_pair.log)
+#ifndef TRT_MESH_PAIRS
+#define TRT_MESH_PAIRS 0
 #endif
 
 __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
@@ -2624,7 +2692,8 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
     const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
     // virtual blocks of the launch: ntiles per frame, or per frame pair (multi-frame launches)
     const uint32_t nvb = A.ntiles * ((!SPLIT && !DEFER && A.nframes > 1u)
-                                         ? (A.xcd_inter && A.frame_group > 1u ? (A.nframes + 1u) / 2u : A.nframes)
+                                         ? (A.xcd_inter && A.frame_group > 1u && (GEOM == 0 || TRT_MESH_PAIRS)
+                                                ? (A.nframes + 1u) / 2u : A.nframes)
                                          : 1u);
     if (vb >= nvb) return;
 #else
@@ -2675,7 +2744,9 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
     // and counting passes launch one frame)
     uint32_t f = 0, t = vb, tile;
     if (!SPLIT && !DEFER && A.nframes > 1u) {
-        if (A.xcd_inter && A.frame_group > 1u) {
+        // frame pairs serve triangle-free frames only (the host sets frame_group 2 for them by
+        // default): mesh kernels do not compile the two extra trace_tile copies (code size)
+        if (A.xcd_inter && A.frame_group > 1u && (GEOM == 0 || TRT_MESH_PAIRS)) {
             // frame pairs: the block traces its tile in frames 2p and 2p + 1 (consecutive frames'
             // tiles cost nearly the same, so the pairs keep the waves balanced) — half the
             // workgroups, so half the per-workgroup launch and slot-refill overhead.  Two calls,
@@ -3479,7 +3550,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     }
     // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)
 #if !defined(TRT_PERSIST) && !defined(TRT_TPW)
-    const uint32_t fblocks = A.nframes > 1u && A.xcd_inter && A.frame_group > 1u ? (A.nframes + 1u) / 2u
+    const uint32_t fblocks = A.nframes > 1u && A.xcd_inter && A.frame_group > 1u && (geom == 0 || TRT_MESH_PAIRS)
+                                 ? (A.nframes + 1u) / 2u
                                                                                   : std::max(A.nframes, 1u);
 #if TRT_WPB == 1
     const dim3 fgrid(A.ntiles * fblocks);

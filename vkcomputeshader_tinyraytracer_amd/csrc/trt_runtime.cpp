@@ -229,7 +229,7 @@ int trt_create(trt_ctx** out, int hip_device) {
         c->defer_in_flight = (uint32_t)std::min((int)TRT_BUILD_MAX_IN_FLIGHT, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_SKEW")) c->xcd_skew = (uint32_t)std::min(7, std::max(0, std::atoi(e)));
-    if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = std::atoi(e) != 0 ? 1u : 0u;
+    if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = (uint32_t)std::min(2, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_FRAME_GROUP")) c->frame_group = std::min(2, std::max(1, std::atoi(e)));
     *out = c;
     return TRT_OK;
@@ -671,6 +671,16 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.xcd_rot = c->xcd_rot;
     A.xcd_skew = c->xcd_skew;
     A.xcd_inter = c->xcd_inter;
+    {   // xcd_inter 2: a multiplier near 0.618 of the dealt chunk count, coprime to it (a
+        // golden-ratio step spreads each XCD's chunks evenly over the image)
+        const uint32_t tyn = (A.rows + 7u) / 8u;
+        const uint32_t nfull = ((A.ntx / 2u) * (tyn / 2u) / 8u) * 8u;
+        uint32_t m = nfull ? (uint32_t)(0.6180339887 * nfull) | 1u : 1u;
+        auto gcd = [](uint32_t a, uint32_t b) { while (b) { const uint32_t t = a % b; a = b; b = t; } return a; };
+        while (nfull && gcd(m, nfull) != 1u) m += 2u;
+        A.xcd_mult = nfull ? m % nfull : 1u;
+        if (A.xcd_mult == 0u || nfull >= 65536u) A.xcd_mult = 1u; // the kernel's k * mult stays in 32 bits
+    }
     // Frame groups (trace_kernel): triangle-free frames (C2) 14.8 -> 13.85 us per frame at
     // 20-frame launches with pairs; mesh frames lose (C4 +2.5 %, C3 +10 %: their tiles' costs
     // vary more from frame to frame and a pair doubles the longest wave),
@@ -1399,6 +1409,23 @@ extern "C" int trt_diag_shadow_batch(trt_ctx* c, const trt_params* p, const void
 // out[1] BVH4 nodes, out[2] quantized (0/1), out[3] compressed (0/1), out[4] worst-case BVH4
 // stack, out[5] leaf triangles.  Returns TRT_ERR_INVALID when no BVH is built (overlapping
 // batch ranges).
+// Diagnostic (tests/test_bvh_layout.py): the BVH2 the upload builds — nodes and the BVH-ordered
+// leaf triangle records (meta: triangle, batch, ni) — copied out when the capacities suffice;
+// counts[0] = nodes, counts[1] = leaf references.
+extern "C" int trt_diag_bvh_export(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
+                                   trt::BvhNode* nodes_out, uint32_t cap_nodes, TriGeo* tris_out, uint32_t cap_tris,
+                                   uint64_t counts[2]) {
+    if (!counts || (ntri && !tris) || (nmodel && !models)) return TRT_ERR_INVALID;
+    std::vector<trt::BvhNode> bvh;
+    std::vector<TriGeo> bvh_tris;
+    if (!nmodel || !trt::build_bvh(tris, ntri, models, nmodel, bvh, bvh_tris)) return TRT_ERR_INVALID;
+    counts[0] = bvh.size();
+    counts[1] = bvh_tris.size();
+    if (nodes_out && bvh.size() <= cap_nodes) std::memcpy(nodes_out, bvh.data(), bvh.size() * sizeof(trt::BvhNode));
+    if (tris_out && bvh_tris.size() <= cap_tris) std::memcpy(tris_out, bvh_tris.data(), bvh_tris.size() * sizeof(TriGeo));
+    return TRT_OK;
+}
+
 extern "C" int trt_diag_bvh_build(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                                   uint64_t out[6]) {
     if (!out || (ntri && !tris) || (nmodel && !models)) return TRT_ERR_INVALID;
