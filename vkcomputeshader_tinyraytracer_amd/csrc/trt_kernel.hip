@@ -154,10 +154,12 @@ __device__ __forceinline__ bool sphere_hit(f3 o, f3 d, const SphereArg& s, float
 // Two spheres' ray_sphere_intersect prologue in packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two
 // IEEE operations per instruction, each rounded as its scalar form, no contraction): L = c - o,
 // tca = dot(L, d), d2 = dot(L, L) - tca * tca in sphere_hit's operand order, so every element is
-// sphere_hit's value bit for bit.  Half the VALU instructions of the four sphere tests of every
-// query (C2: ~2.9 queries per pixel).
+// sphere_hit's value bit for bit.
+// Measured and rejected (round 5): in scene_intersect alone C2 +5 % (12.8 vs 12.2 us per frame at
+// 20-frame launches, profiles/r05i_ab_sphere_pk.jsonl: the packed operands cost register moves
+// and pairs at the 96-VGPR cap); in shadow_intersect it spills the C2 kernel (60 B).
 #ifndef TRT_SPHERE_PK
-#define TRT_SPHERE_PK 1 /* bit 0: scene_intersect, bit 1: shadow_intersect (spills the C2 kernel: 60 B) */
+#define TRT_SPHERE_PK 0 /* bit 0: scene_intersect, bit 1: shadow_intersect */
 #endif
 typedef float pk2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void sphere_pair_pre(f3 o, f3 d, const SphereArg& s0, const SphereArg& s1, pk2& tca, pk2& d2) {
