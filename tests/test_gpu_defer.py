@@ -238,3 +238,33 @@ def test_count_frames_keep_reference_counters(gpu_renderer, scenes):
     _, _, ost = orc.render(sc, sc.params())
     for k in T.Stats.EXACT:
         assert gst[k] == ost[k], k
+
+
+@pytest.mark.parametrize("ppw", ["16", "32", "64"])
+def test_pass_a_pixels_per_wave(scenes, ppw):
+    """TRT_DEFER_PPW: pass A with 64 / 32 / 16 pixels per wave (1, 2, 4 waves per 8x8 tile, the
+    other lanes fed by the wave's segment pool) — the frame is the unsplit loop's bit for bit
+    (the automatic choice, 2 waves per tile at <= 4 frames in flight, is what trt_render runs)."""
+    import os
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    old = os.environ.get("TRT_DEFER_PPW")
+    os.environ["TRT_DEFER_PPW"] = ppw
+    try:
+        r = trt.Renderer(0)
+    finally:
+        if old is None:
+            os.environ.pop("TRT_DEFER_PPW", None)
+        else:
+            os.environ["TRT_DEFER_PPW"] = old
+    try:
+        for name in ("ref", "readme"):
+            sc = scenes[name]
+            r.upload_scene(sc)
+            d8, d32 = _frame(r, sc, DEFER_ON)
+            u8, u32 = _frame(r, sc, DEFER_OFF)
+            assert np.array_equal(d8, u8) and np.array_equal(d32, u32), name
+            assert r.defer_stats(0)["fallback_pixels"] == 0
+    finally:
+        r.close()

@@ -29,6 +29,8 @@ for v in "$@"; do
         oldsize) variant oldsize -DTRT_LIGHT_UNROLL=1 -DTRT_MESH_PAIRS=1 ;;
         sh4) variant sh4 -DTRT_G3_WAVES_SHALLOW=4 ;;
         pk0) variant pk0 -DTRT_SPHERE_PK=0 ;;
+        park1) variant park1 -DTRT_G3_PARK=1 ;;
+        unroll) variant unroll -DTRT_LIGHT_UNROLL=1 ;;
         lds24) variant lds24 -DTRT_G3_LDS=24 ;;
         lds32) variant lds32 -DTRT_G3_LDS=32 ;;
         cur) variant cur ;;

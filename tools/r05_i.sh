@@ -39,3 +39,11 @@ for l in open(sys.argv[1]):
         r = json.loads(l); d[r['tag']].append((r['wall_us_no_events'], r['med_us']))
 for k in sorted(d): print(k, 'wall us/frame', [x[0] for x in d[k]], 'span us', [x[1] for x in d[k]])
 PY
+cd /tmp
+for cf in "C4 4" "C3 20" "ref 4"; do
+  set -- $cf
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/pmc_$1_$ctr" -o run -- python "$ROOT/tools/kbench.py" --config $1 --frames $2 --settle-ms 0 --inflight 1 > "$OUT/pmc_$1_$ctr.log" 2>&1 || { tail -5 "$OUT/pmc_$1_$ctr.log"; exit 1; }
+  done
+done
+echo pmc done

@@ -77,6 +77,10 @@ struct trt_ctx {
     // TRT_DEFER_LEVELS (breadth first, inline shadow rays), TRT_DEFER_LEVELS_B (breadth first,
     // shadow rays in pass B).  TRT_DEFER_MODE env: "pool" / "levels" / "levels_b".
     int defer_design = TRT_DEFER_POOL;
+    // pass-A waves per tile of the pool design: 0 = auto (2 when <= 4 frames overlap, else 1),
+    // TRT_DEFER_PPW = 64 / 32 / 16 pixels per wave forces 1 / 2 / 4
+    uint32_t defer_sub = 0;
+    uint32_t cur_in_flight = 1; // frames in flight of the current render call
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.

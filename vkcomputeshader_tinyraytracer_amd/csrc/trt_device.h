@@ -300,6 +300,7 @@ struct KArgs {
     uint2* __restrict__ px_ev;        // per output pixel: (root event slot or kEvNone, 0)
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
+    uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4: trace_tile)
     // deferred frames, level mode (lv != 0): see LevCtr
     uint32_t lv;                      // level mode: 1 = shadow rays inline, 2 = shadows in pass B
     uint32_t lv_level;                // the depth this launch traces (level_kernel)

@@ -2475,20 +2475,27 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, const FrameRec& F, s
 // One 8x8 pixel tile of compact output rows: the wave's 64 lanes, one pixel each.  SPLIT
 // (spp == 1 only): a pixel whose tree handed subtrees to the task queue parks its partial
 // colour in A.acc and is finished by finalize_spilled.
+// DEFER: pass A with A.defer_sub > 1 gives each tile defer_sub waves (sub = 0 .. defer_sub - 1):
+// wave `sub` starts with 64 / defer_sub of the tile's pixels (rows sub * 8 / defer_sub ...) and
+// its other lanes take work from the wave's segment pool as the trees grow, so a glass tile's
+// segments are spread over more waves (a shorter frame latency) at the price of idle lanes in
+// cheap tiles.
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
 __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, uint32_t tile, Cnt& cnt, float* lds,
-                                           float4* slab) {
+                                           float4* slab, uint32_t sub = 0) {
     const uint32_t lane = lane_id();
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
-    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
+    uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
     if constexpr (DEFER) { // pass A of a deferred-shadow frame (spp == 1): every lane walks
-        const bool valid = x < A.width && k < A.rows;
+        const uint32_t S = A.defer_sub > 1u ? A.defer_sub : 1u, rows = 8u / S;
+        k = (tile / A.ntx) * 8u + sub * rows + (lane >> 3);
+        const bool valid = x < A.width && k < A.rows && (lane >> 3) < rows;
         EvLog L;
         // multiplicative hash of the tile: a frame's costly region (a glass object) spans few
         // tile columns, so tile % stripes would pile its queries into a few stripes
-        L.stripe = (tile * 0x9E3779B1u) >> (32 - 7);
+        L.stripe = ((tile * S + sub) * 0x9E3779B1u) >> (32 - 7);
         static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
         const size_t o = valid ? (size_t)k * A.width + x : 0u;
         const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
@@ -2768,6 +2775,10 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
             t = vb - f * A.ntiles;
             tile = xcd_tile(A, t, f);
         }
+    } else if (DEFER && !SPLIT && A.defer_sub > 1u) { // defer_sub waves per tile (trace_tile)
+        tile = xcd_tile(A, t / A.defer_sub);
+        trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % A.defer_sub);
+        return;
     } else {
         tile = xcd_tile(A, t);
     }
@@ -3421,7 +3432,8 @@ static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
                                dim3(64), 0, stream, A);
         }
     } else {
-        hipLaunchKernelGGL((trace_kernel<0, false, GEOM, false, true, false>), grid, block, 0, stream, A);
+        const uint32_t S = A.defer_sub > 1u ? A.defer_sub : 1u;
+        hipLaunchKernelGGL((trace_kernel<0, false, GEOM, false, true, false>), dim3(grid.x * S), block, 0, stream, A);
     }
     // persistent: up to 8 waves per SIMD (the shadow-only kernel is light on VGPRs and LDS;
     // waves that find the queue drained exit at once)

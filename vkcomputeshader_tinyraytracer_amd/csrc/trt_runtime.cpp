@@ -225,6 +225,10 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (const char* e = std::getenv("TRT_DEFER_MODE"))
         c->defer_design = std::strcmp(e, "levels") == 0 ? TRT_DEFER_LEVELS
                           : std::strcmp(e, "levels_b") == 0 ? TRT_DEFER_LEVELS_B : TRT_DEFER_POOL;
+    if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32 or 16
+        const int ppw = std::atoi(e);
+        c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
+    }
     if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT"))
         c->defer_in_flight = (uint32_t)std::min((int)TRT_BUILD_MAX_IN_FLIGHT, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
@@ -875,6 +879,12 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     b.last_levels = design == TRT_DEFER_LEVELS;
     b.last_npx = npx;
     A.defer = 1;
+    // pass-A waves per tile (pool design): explicit (TRT_DEFER_PPW), else by the frames that
+    // overlap: with few frames in flight a frame's latency — its deepest tile's chain of
+    // segments — sets the rate, and two waves per tile halve that chain (the shipped frame at 2
+    // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
+    // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
+    A.defer_sub = c->defer_sub ? c->defer_sub : (c->cur_in_flight <= 4u ? 2u : 1u);
     A.lv = design == TRT_DEFER_LEVELS ? 1u : design == TRT_DEFER_LEVELS_B ? 2u : 0u;
     A.lv_level = 0;
     // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
@@ -1052,6 +1062,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
         }
     }
     uint32_t nfl = std::min(want, nl);
+    c->cur_in_flight = nfl;
     std::vector<hipStream_t> sv{c->stream};
     // every slot's stream is made on first use of the in-flight count, not only the ones this
     // call needs: creating a stream takes milliseconds and must not land in a later, longer
@@ -1086,6 +1097,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
             if (c->frames_in_flight || slot == 0) return rc;
             c->err.clear();
             nfl = slot;
+            c->cur_in_flight = nfl;
             slot = j % nfl;
             if ((rc = prepare_split(c, p, A, slot, sv[slot])) != TRT_OK) return rc;
         }
@@ -1194,6 +1206,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
         }
     }
     const uint32_t slot = render_slot(c, c->stream);
+    c->cur_in_flight = 1u; // one frame: its latency is the rate
     if ((rc = prepare_split(c, p, A, slot, c->stream)) != TRT_OK) return rc;
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 32 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
