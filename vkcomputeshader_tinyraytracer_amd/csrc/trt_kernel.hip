@@ -2489,7 +2489,8 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
     uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
     if constexpr (DEFER) { // pass A of a deferred-shadow frame (spp == 1): every lane walks
-        const uint32_t S = A.defer_sub > 1u ? A.defer_sub : 1u, rows = 8u / S;
+        // (split launches keep one wave per tile: their grid is the tile count)
+        const uint32_t S = (!SPLIT && A.defer_sub > 1u) ? A.defer_sub : 1u, rows = 8u / S;
         k = (tile / A.ntx) * 8u + sub * rows + (lane >> 3);
         const bool valid = x < A.width && k < A.rows && (lane >> 3) < rows;
         EvLog L;
