@@ -650,14 +650,11 @@ def measure_traffic(args, kernel_us_per_frame: float | None, table_key: str | No
     """Memory-side bytes per frame of the dominant kernel, from two separate PMC passes
     (FETCH_SIZE, WRITE_SIZE; MI355X_MICROARCH.md §HBM: the two cannot share a pass) over a child
     run of the line's own frame loop; the launches of the timed size (the largest grid) are kept.
-    FETCH_SIZE and WRITE_SIZE are KiB.  The guide's gfx950 note (FETCH_SIZE counts HALF the bytes
-    of a wide coalesced STREAMING read) was calibrated here for this tracer's own pattern
-    (tools/calib/fetch_calib.hip, profiles/r05i_fetch_calibration.log): a 16-B gather that is the
-    only access to its 64-B block is one 64-B request counted as 64 B, and the two halves of a
-    line are two requests — so for gathers (envmap footprints, BVH nodes, triangles) FETCH_SIZE is
-    the bytes moved, while a stream (the calibration's own offset array) is counted at 1/2.  The
-    trace kernels read by gathers only, so traffic = FETCH + WRITE; the streaming-corrected
-    2 x FETCH + WRITE is kept beside it as an upper bound."""
+    FETCH_SIZE and WRITE_SIZE are KiB.  The guide's gfx950 note (FETCH_SIZE counts half the bytes
+    of a wide coalesced streaming read) holds for this tracer's gathers too: calibrated with
+    tools/calib/fetch_calib.hip (profiles/r05j_fetch_calibration_aligned.log), every 128-B line a
+    dispatch touches is ONE request counted as 64 B, whether one 16-B lane, both 64-B halves or
+    all 128 B of it are read.  So traffic = 2 x FETCH + WRITE (the raw figures are kept beside it)."""
     import shutil
     import tempfile
 
@@ -693,10 +690,9 @@ def measure_traffic(args, kernel_us_per_frame: float | None, table_key: str | No
             return out or None
         out.update({"source": f"table: {TRAFFIC_TABLE.relative_to(REPO)} ({t.get('measured', '')})",
                     "fetch_bytes_raw": t["fetch_bytes_raw"], "write_bytes": t["write_bytes"]})
-    out["bytes_per_frame"] = out["fetch_bytes_raw"] + out["write_bytes"]
-    out["bytes_per_frame_if_streaming"] = 2 * out["fetch_bytes_raw"] + out["write_bytes"]
-    out["fetch_correction"] = ("x1: gathers are counted at their 64-B request size (tools/calib/fetch_calib.hip); "
-                               "x2 applies to streaming reads only")
+    out["bytes_per_frame"] = 2 * out["fetch_bytes_raw"] + out["write_bytes"]
+    out["fetch_correction"] = ("x2: each 128-B line read is one request counted as 64 B, for streams and for this "
+                               "kernel's gathers alike (tools/calib/fetch_calib.hip)")
     if kernel_us_per_frame:
         gbs = out["bytes_per_frame"] / (kernel_us_per_frame * 1e-6) / 1e9
         out["hbm_gb_s"] = round(gbs, 1)
@@ -882,8 +878,8 @@ def main():
                       "traces many frames), from a second, untimed pass of the same loop.  Peak counts an FMA "
                       "as 2 flops; the kernel has no FMA contraction "
                       "(-ffp-contract=off).  traffic: memory-side bytes per frame of trace_kernel from PMC "
-                      "(FETCH_SIZE + WRITE_SIZE: FETCH_SIZE counts gathers at their 64-B request size, calibrated "
-                      "in tools/calib/fetch_calib.hip; see traffic_detail)")
+                      "(2 x FETCH_SIZE + WRITE_SIZE: a 128-B line read is one request counted as 64 B, calibrated "
+                      "for this kernel's gathers in tools/calib/fetch_calib.hip; see traffic_detail)")
         if not dist_mode:
             # over the kernel time per frame, or the wall time per frame when the event pass's
             # span is not the shorter one (then the rate is a lower bound)

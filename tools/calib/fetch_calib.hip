@@ -11,9 +11,13 @@
 //   4 gather16 : the envmap-like pattern: 16 B per lane, lanes of a wave spread over 8 lines
 //                8 lanes per line at 16-B steps (128 B of each line read)
 // Prints the bytes each dispatch requested; rocprofv3 gives FETCH_SIZE per dispatch.  Every
-// dispatch also streams its offset array (8 B per lane, coalesced): FETCH_SIZE counts that stream
-// at half its bytes (the guide's gfx950 note), which the analysis subtracts.
-// Regions start on 4-KiB boundaries.
+// dispatch also streams its offset array (8 B per lane, coalesced), counted at half its bytes,
+// which the analysis subtracts.  Regions start on 4-KiB boundaries.  Result
+// (profiles/r05j_fetch_calibration_aligned.log): patterns 1-4 are each one 64-B-counted request
+// per 128-B line touched (sparse128, pair128 — both halves of a line — and sparse64 alike, and
+// gather16 reading all 128 B), i.e. FETCH_SIZE = half of the lines' bytes for gathers as for
+// streams.  (A first run with regions misaligned to 128 B, profiles/r05i_fetch_calibration.log,
+// put the pair's halves on two lines and read as if each half were its own request.)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
