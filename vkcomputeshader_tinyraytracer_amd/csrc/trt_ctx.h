@@ -81,6 +81,7 @@ struct trt_ctx {
     // TRT_DEFER_PPW = 64 / 32 / 16 pixels per wave forces 1 / 2 / 4
     uint32_t defer_sub = 0;
     uint32_t cur_in_flight = 1; // frames in flight of the current render call
+    bool spp_lanes = true;      // spp > 1 frames: one lane per sample (TRT_SPP_LANES)
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.

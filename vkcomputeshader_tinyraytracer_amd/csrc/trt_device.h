@@ -301,6 +301,7 @@ struct KArgs {
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
     uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4: trace_tile)
+    uint32_t spp_lanes;               // spp > 1: one lane per sample (trace_samples), spp waves per tile
     // deferred frames, level mode (lv != 0): see LevCtr
     uint32_t lv;                      // level mode: 1 = shadow rays inline, 2 = shadows in pass B
     uint32_t lv_level;                // the depth this launch traces (level_kernel)

@@ -2555,6 +2555,44 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
     store_pixel(A, F, o, acc);
 }
 
+// spp > 1 with one lane per SAMPLE (A.spp_lanes; spp a power of two in [2, 64]).  Wave `sub` of
+// 8x8 tile `tile` traces the 64 / spp pixels of sub-block `sub` (2x2 pixels at 16 spp), spp lanes
+// per pixel: the 16 jittered samples of a pixel are nearly one ray, so a wave's walks are far
+// more coherent than 64 neighbouring pixels' (the wave-uniform node fetch fires more often) and
+// the wave-coherent shadow walk applies to all of them.  The pixel's colour is then the
+// per-pixel loop's running sum, ((0 + c0) + c1) + ..., gathered from its lanes in sample order
+// with the same additions, and divided by spp — bit-identical to trace_tile's loop.
+template <int CAP, bool COUNT, int GEOM>
+__device__ __forceinline__ void trace_samples(const KArgs& A, const FrameRec& F, uint32_t tile, uint32_t sub, Cnt& cnt,
+                                              float* lds, float4* slab) {
+    const uint32_t lane = lane_id();
+    if (tile >= A.ntiles) return;
+    const uint32_t spp = A.spp, lg = 31u - __builtin_clz(64u / spp); // log2 of the pixels per wave
+    const uint32_t bw = 1u << ((lg + 1u) / 2u), bh = (64u / spp) / bw;  // sub-block of bw x bh pixels
+    const uint32_t cols = 8u / bw;
+    const uint32_t pi = lane / spp, smp = lane % spp;
+    const uint32_t x = (tile % A.ntx) * 8u + (sub % cols) * bw + pi % bw;
+    const uint32_t k = (tile / A.ntx) * 8u + (sub / cols) * bh + pi / bw;
+    const bool valid = x < A.width && k < A.rows;
+    f3 c = mk(0.0f, 0.0f, 0.0f);
+    if (valid) {
+        const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
+        c = cast_ray<CAP, COUNT, GEOM>(A, orig, primary_dir(A, x, band_row(A, k), smp), cnt, lds, slab);
+        cnt.pri += 1;
+    }
+    // the sample-order sum, gathered by every lane from its pixel's lanes (lane base + t holds
+    // sample t); lanes of invalid pixels gather their (zero) colours and store nothing
+    const int base = (int)(lane - smp);
+    f3 acc = mk(0.0f, 0.0f, 0.0f);
+    for (uint32_t t = 0; t < spp; ++t) {
+        const int src = base + (int)t;
+        acc = add(acc, mk(__shfl(c.x, src, 64), __shfl(c.y, src, 64), __shfl(c.z, src, 64)));
+    }
+    if (!valid || smp != 0u) return;
+    acc = mk(div_rn(acc.x, (float)spp), div_rn(acc.y, (float)spp), div_rn(acc.z, (float)spp));
+    store_pixel(A, F, (size_t)k * A.width + x, acc);
+}
+
 // Blocks b and b+8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md): give each XCD
 // 2x2-tile chunks (16x16 px) so neighbouring pixels' envmap texels and batch records hit
 // the same XCD L2.  Chunk c of XCD x is global chunk c*8+x; chunks are row-major over the
@@ -2753,6 +2791,14 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
     // frame f = vb / ntiles of a multi-frame launch (plain frames only: split / deferred frames
     // and counting passes launch one frame)
     uint32_t f = 0, t = vb, tile;
+    if (!SPLIT && !DEFER && A.spp_lanes) { // one lane per sample: ntiles * spp waves per frame
+        const uint32_t per = A.ntiles * A.spp;
+        f = vb / per;
+        const uint32_t r = vb - f * per;
+        trace_samples<CAP, COUNT, GEOM>(A, A.fr[f], xcd_tile(A, r / A.spp), r % A.spp, cnt, lds, slab);
+        if (COUNT) flush_counts(A, cnt);
+        return;
+    }
     if (!SPLIT && !DEFER && A.nframes > 1u) {
         // frame pairs serve triangle-free frames only (the host sets frame_group 2 for them by
         // default): mesh kernels do not compile the two extra trace_tile copies (code size)
@@ -3565,9 +3611,10 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     }
     // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)
 #if !defined(TRT_PERSIST) && !defined(TRT_TPW)
-    const uint32_t fblocks = A.nframes > 1u && A.xcd_inter && A.frame_group > 1u && (geom == 0 || TRT_MESH_PAIRS)
+    const uint32_t fblocks = A.spp_lanes ? std::max(A.nframes, 1u) * A.spp
+                             : A.nframes > 1u && A.xcd_inter && A.frame_group > 1u && (geom == 0 || TRT_MESH_PAIRS)
                                  ? (A.nframes + 1u) / 2u
-                                                                                  : std::max(A.nframes, 1u);
+                                 : std::max(A.nframes, 1u);
 #if TRT_WPB == 1
     const dim3 fgrid(A.ntiles * fblocks);
 #else // TRT_WPB waves per workgroup: virtual blocks as in trace_kernel, whole groups of 8 blocks

@@ -225,6 +225,7 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (const char* e = std::getenv("TRT_DEFER_MODE"))
         c->defer_design = std::strcmp(e, "levels") == 0 ? TRT_DEFER_LEVELS
                           : std::strcmp(e, "levels_b") == 0 ? TRT_DEFER_LEVELS_B : TRT_DEFER_POOL;
+    if (const char* e = std::getenv("TRT_SPP_LANES")) c->spp_lanes = std::atoi(e) != 0;
     if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32 or 16
         const int ppw = std::atoi(e);
         c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
@@ -636,6 +637,9 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     A.band_index = p->band_index;
     A.max_depth = p->max_depth;
     A.spp = p->spp ? p->spp : 1;
+    // spp a power of two in [2, 64] and no replayed rays: one lane per sample (trace_samples;
+    // TRT_SPP_LANES=0 keeps the per-pixel sample loop)
+    A.spp_lanes = (A.spp >= 2u && A.spp <= 64u && (A.spp & (A.spp - 1u)) == 0u && !p->rays_in && c->spp_lanes) ? 1u : 0u;
     A.seed = p->seed;
     A.flags = p->flags;
     // dir_z = -1.0 * (HEIGHT / (2.0 * tan(fov / 2.0))) in double, main.cpp:1503
