@@ -34,6 +34,8 @@ for v in "$@"; do
         lds24) variant lds24 -DTRT_G3_LDS=24 ;;
         lds32) variant lds32 -DTRT_G3_LDS=32 ;;
         cur) variant cur ;;
+        late0) variant late0 -DTRT_LATE_MAT=0 ;;
+        sh4late) variant sh4late -DTRT_G3_WAVES_SHALLOW=4 ;;
         g3p24) variant g3p24 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=24 ;;
         g3p32) variant g3p32 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=32 ;;
         g3p16) variant g3p16 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=16 ;;

@@ -1776,6 +1776,53 @@ __device__ __forceinline__ void make_children(const Seg& cur, const Surf& s, int
     }
 }
 
+// TRT_LATE_MAT (mesh kernels, GEOM >= 2, per-pixel loop): the light loop runs in three phases
+// -- the three lights' diffuse / specular terms, then the shadow walks, then the lit terms summed
+// in light order -- and the material (albedo weights, kd, index of refraction) is fetched again
+// after the walks instead of being held across them.  Across a walk the lane keeps the hit
+// point, normal, direction, colour, throughput, depth, the hit's kind and index and the six
+// terms, not the eleven material floats the 96-VGPR build spilled to scratch.  Same operations
+// in the same order: bit-identical.
+#ifndef TRT_LATE_MAT
+#define TRT_LATE_MAT 1
+#endif
+struct MatVals {
+    float alb[4], kd[3], sexp, ior;
+};
+__device__ __forceinline__ MatVals load_mat(const KArgs& A, int kind, int idx, f3 p) {
+    MatVals m;
+    if (kind == HIT_FLOOR) {
+        float c0 = 0.3f, c1 = 0.3f, c2 = 0.3f;
+        if (A.flags & TRT_FLAG_CHECKER) { // shader.comp:312
+            float q = floorf(p.x * 0.5f + 1024.0f) + floorf(p.z * 0.5f);
+            float mod2 = q - 2.0f * floorf(q / 2.0f);
+            if (!(mod2 == 0.0f)) {
+                c1 = 0.2f;
+                c2 = 0.1f;
+            }
+        }
+        m.alb[0] = 2.0f; m.alb[1] = 0.0f; m.alb[2] = 0.0f; m.alb[3] = 0.0f;
+        m.kd[0] = c0; m.kd[1] = c1; m.kd[2] = c2;
+        m.sexp = 1.0f;
+        m.ior = 1.0f;
+    } else if (kind == HIT_SPHERE) {
+        const Mat& mm = A.sph[idx].m;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m.alb[k] = mm.albedo[k];
+        m.kd[0] = mm.kd[0]; m.kd[1] = mm.kd[1]; m.kd[2] = mm.kd[2];
+        m.sexp = mm.spec_exp;
+        m.ior = mm.ior;
+    } else {
+        const Mat& mm = A.mats[A.shade[idx].material];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m.alb[k] = mm.albedo[k];
+        m.kd[0] = mm.kd[0]; m.kd[1] = mm.kd[1]; m.kd[2] = mm.kd[2];
+        m.sexp = mm.spec_exp;
+        m.ior = mm.ior;
+    }
+    return m;
+}
+
 // The DFS of one segment tree (root = a primary ray, or a task of a split launch).  Returns
 // the unclamped colour sum in the reference's pop order.  SPLIT: children at depth
 // >= A.split_d1 are handed to the task queue (`spilled` is set) instead of being traced.
@@ -1867,11 +1914,74 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             // Phong with three shadow rays, shader.comp:483-507.
             f3 v = neg(cur.d);
             f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
-            f3 kdv = mk(kd[0], kd[1], kd[2]);
+            constexpr bool LATE = GEOM >= 2 && TRT_LATE_MAT && !HYB && !park_state<GEOM, HYB>();
+            if constexpr (LATE) {
+                // Phase 1: the three lights' terms (light_term's arithmetic), before any walk.
+                float dif[3], spc[3];
+                uint32_t need = 0u;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
+                    float dist;
+                    f3 ld = normalize_len3(sub(L, p), dist);
+                    dif[i] = 1.0f * fmaxf(0.0f, dot3(n, ld));
+                    spc[i] = 0.0f;
+                    if (!TRT_SPEC_SKIP || alb[1] != 0.0f) {
+                        const f3 rdir = reflect3(neg(ld), n);
+#ifdef TRT_DIAG_NO_POW
+                        spc[i] = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp;
+#else
+                        spc[i] = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
+#endif
+                    }
+                    const bool matters = TRT_SKIP_DARK == 0 || (alb[0] != 0.0f && dif[i] != 0.0f) ||
+                                         (alb[1] != 0.0f && spc[i] != 0.0f);
+                    need |= (matters ? 1u : 0u) << i;
+                }
+                // Phase 2: the shadow walks (the loop stays rolled: one inlined walk).
+                uint32_t lit = 0u;
+                for (int i = 0; i < 3; ++i) {
+                    if (COUNT) ++cnt.sh;
+                    const bool matters = (need >> i) & 1u;
+                    if (!COUNT && !matters) continue;
+                    f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
+                    float dist;
+                    f3 ld = normalize_len3(sub(L, p), dist);
+                    f3 so = dot3(ld, n) < 0.0f ? sub(p, muls(n, TRT_EPS)) : add(p, muls(n, TRT_EPS));
+                    const Cnt before = cnt;
+                    const bool occl = shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab);
+                    if (COUNT && !matters) {
+                        ++cnt.sk;
+                        cnt.ssph += cnt.sph - before.sph;
+                        cnt.sbox += (cnt.nt + cnt.bt) - (before.nt + before.bt);
+                        cnt.stt += cnt.tt - before.tt;
+                        cnt.sta += cnt.ta - before.ta;
+                        cnt.stu += cnt.tu - before.tu;
+                        cnt.stv += cnt.tv - before.tv;
+                    }
+                    if (!occl) lit |= 1u << i;
+                }
+                // Phase 3: the material again (an opaque index: not the pre-walk registers).
+                int hk = h.kind, hi = h.idx;
+                asm volatile("" : "+v"(hk), "+v"(hi));
+                const MatVals mv = load_mat(A, hk, hi, p);
+                const f3 kdv2 = mk(mv.kd[0], mv.kd[1], mv.kd[2]);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (!((lit >> i) & 1u)) continue;
+                    diffuse = add(diffuse, muls(kdv2, dif[i]));
+                    specular = add(specular, muls(kdv2, spc[i]));
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) alb[k] = mv.alb[k];
+                ior = mv.ior;
+            }
             // PARK (GEOM 3): what the light loop does not need during its shadow walks waits in
             // this lane's LDS column (park_state) and is read back after each walk / the loop.
             constexpr bool PARK = park_state<GEOM, HYB>();
             lds_f32* const P = (lds_f32*)(lds + lane_id());
+            if constexpr (!LATE) {
+            f3 kdv = mk(kd[0], kd[1], kd[2]);
             if constexpr (PARK) {
                 const float f[kParkFields] = {color.x, color.y, color.z, cur.thr, __int_as_float(cur.depth), alb[2],
                                               alb[3], ior, cur.d.x, cur.d.y, cur.d.z, kd[0], kd[1], kd[2], sexp, alb[0]};
@@ -1946,6 +2056,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 diffuse = add(diffuse, muls(kd_i, diff));
                 specular = add(specular, muls(kd_i, spec));
             }
+            } // !LATE
             if constexpr (PARK) {
                 park_fence();
                 color = mk(P[0], P[64], P[128]);
