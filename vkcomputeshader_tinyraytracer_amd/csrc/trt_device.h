@@ -268,6 +268,7 @@ struct KArgs {
     uint32_t ntx;                     // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
     uint32_t bvh_waves4;          // BVH walk: the 4-waves-per-SIMD build (GEOM 3)
+    uint32_t bvh4q_n;             // nodes of bvh4q (the walk's LDS copy of the top nodes)
     uint32_t xcd_rot, xcd_skew;   // multi-frame tile dealing (xcd_tile): rotation period, row skew
     uint32_t xcd_inter;           // ... frames interleaved per chunk group (inter_tile); 2: no rotation, permuted classes
     uint32_t xcd_mult;            // ... xcd_inter 2: chunk permutation multiplier (coprime to the dealt chunks)

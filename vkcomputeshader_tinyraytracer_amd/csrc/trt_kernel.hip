@@ -418,6 +418,31 @@ constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS :
 // 32-bit words of a wave's BVH-stack LDS (slab_float4s below holds them)
 template <int GEOM>
 constexpr int slab_words() { return bvh_lds_entries<GEOM>() * 64; }
+// TRT_TOP_LDS: the wave keeps the first K nodes of the quantized BVH4 in its LDS (the nodes are
+// numbered breadth first: the root, its children, their children: K = 21 is the top three
+// levels of a full tree), copied once when the wave starts; a lane whose walk stands on one of
+// them reads it with ds_read_b128 instead of four per-lane global loads through TA / TD (the
+// walk is bound by the vector-memory pipe).  Wave-uniform visits keep their scalar fetch.
+// The slab holds, after the traversal stack, one header float4 (x = the nodes copied) and the
+// nodes; every kernel with a GEOM 3 slab fills it (top_fill) before its first walk.
+// Measured and rejected (round 5, profiles/r05r_ab_top_lds.jsonl, same box, two rounds): K = 21
+// C4 +0.6 %, C3 +2 %, C5 +0.6 %, the shipped frame +3 %, the README scene +7 %; K = 5 within
+// +-1.5 % of none.  The top levels' visits are mostly wave-uniform (one scalar fetch already),
+// and the extra LDS and the per-lane LDS / global select cost more than the TA / TD cycles the
+// divergent top visits save.  Off (0 compiles it out).
+#ifndef TRT_TOP_LDS
+#define TRT_TOP_LDS 0
+#endif
+// pass A of deferred frames (4 waves per SIMD with the 5-KB segment pool): the top two levels
+// only; split launches (LDS segment stacks) keep none
+#ifndef TRT_TOP_LDS_DEFER
+#define TRT_TOP_LDS_DEFER 5
+#endif
+template <int GEOM, bool DEFER = false>
+constexpr int top_nodes() { return GEOM == 3 ? (DEFER ? TRT_TOP_LDS_DEFER : TRT_TOP_LDS) : 0; }
+// float4 offset of the header in a GEOM 3 slab
+template <int GEOM>
+constexpr int top_off() { return bvh_lds_entries<GEOM>() * 16; }
 
 // PUSH3: the branch-free push of up to three children (push_sorted) — used by the 3-wave
 // build: C3 -4 %, shipped frame -6 %; the 4-wave build (128-VGPR cap) is 3 % slower with it
@@ -894,6 +919,10 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 #endif
             if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) return;
         }
+        // nodes below ntop are in the wave's LDS (top_fill; 0 when the kernel keeps none)
+        uint32_t ntop = 0u;
+        if constexpr (GEOM == 3 && TRT_TOP_LDS > 0)
+            ntop = __builtin_amdgcn_readfirstlane(((const lds_u32*)reinterpret_cast<uint32_t*>(slab + top_off<GEOM>()))[0]);
         auto fetch = [&](uint32_t nd, float4& pe, uint4& qa, uint4& qb, uint4& ch) {
 #if TRT_UNIFORM_NODE == 2
             // the first lane's node through scalar loads for every lane standing on it, the
@@ -928,6 +957,14 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
                 return;
             }
 #endif
+            if (GEOM == 3 && TRT_TOP_LDS > 0 && nd < ntop) {
+                const lds_u32* t = (const lds_u32*)reinterpret_cast<uint32_t*>(slab + top_off<GEOM>() + 1u + nd * 4u);
+                pe = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]), __uint_as_float(t[3]));
+                qa = make_uint4(t[4], t[5], t[6], t[7]);
+                qb = make_uint4(t[8], t[9], t[10], t[11]);
+                ch = make_uint4(t[12], t[13], t[14], t[15]);
+                return;
+            }
             const float4* p = reinterpret_cast<const float4*>(A.bvh4q + nd);
             pe = p[0];
             qa = reinterpret_cast<const uint4*>(p)[1];
@@ -2812,9 +2849,31 @@ __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
     }
 }
 
-template <int GEOM>
+template <int GEOM, int TOP = top_nodes<GEOM>()>
 constexpr int slab_float4s() {
-    return GEOM == 1 ? 64 * 3 : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
+    return GEOM == 1 ? 64 * 3
+         : GEOM == 3 ? top_off<GEOM>() + (TRT_TOP_LDS > 0 ? 1 + 4 * TOP : 0)
+         : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
+}
+// Copies the first min(TOP, nodes) quantized nodes into the slab after the traversal stack and
+// writes their count to the header (trace_bvh4); every lane of the wave calls it.
+template <int GEOM, int TOP = top_nodes<GEOM>()>
+__device__ __forceinline__ void top_fill(const KArgs& A, float4* slab) {
+    if constexpr (GEOM == 3 && TRT_TOP_LDS > 0) {
+        lds_u32* t = (lds_u32*)reinterpret_cast<uint32_t*>(slab + top_off<GEOM>());
+        const uint32_t n = A.bvh4q ? min((uint32_t)TOP, A.bvh4q_n) : 0u;
+        if (lane_id() == 0u) t[0] = n;
+        const uint4* src = reinterpret_cast<const uint4*>(A.bvh4q);
+        for (uint32_t i = lane_id(); i < n * 4u; i += 64u) {
+            const uint4 v = src[i];
+            lds_u32* d = t + 4u * (1u + i);
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+        wave_lds_sync();
+    }
 }
 // Triangle-free frames (GEOM 0: C1 / C2) are latency-bound on the dependent chain intersection
 // -> shading -> envmap gather; 5 waves per SIMD (<= 96 VGPRs) hide more of it than the 4 the
@@ -2844,10 +2903,10 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
     // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
     // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
     __shared__ float lds_all[(DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>()) * TRT_WPB];
-    __shared__ float4 slab_all[slab_float4s<GEOM>() * TRT_WPB];
+    __shared__ float4 slab_all[slab_float4s<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>() * TRT_WPB];
     const uint32_t w = threadIdx.x >> 6;
     float* lds = lds_all + w * (DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>());
-    float4* slab = slab_all + w * slab_float4s<GEOM>();
+    float4* slab = slab_all + w * slab_float4s<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>();
     const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
     // virtual blocks of the launch: ntiles per frame, or per frame pair (multi-frame launches)
     const uint32_t nvb = A.ntiles * ((!SPLIT && !DEFER && A.nframes > 1u)
@@ -2858,9 +2917,10 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
 #else
     __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>()];
     // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
-    __shared__ float4 slab[slab_float4s<GEOM>()];
+    __shared__ float4 slab[slab_float4s<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>()];
     const uint32_t vb = blockIdx.x;
 #endif
+    top_fill<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>(A, slab);
     Cnt cnt;
 #ifdef TRT_DIAG_WAVE_CLOCK
     // diagnostic: per-workgroup (tile | xcc << 28, start lo, duration, start hi) of the
@@ -2976,7 +3036,8 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
 template <int CAP, bool COUNT, int GEOM, bool DEFER = false>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs A) {
     __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, true>()];
-    __shared__ float4 slab[slab_float4s<GEOM>()];
+    __shared__ float4 slab[slab_float4s<GEOM, 0>()];
+    top_fill<GEOM, 0>(A, slab); // split tasks: no node copy (their LDS goes to segment stacks)
     Cnt cnt;
     const uint32_t n = min(*A.q_in_n, A.q_cap);
     // static schedule: wave b takes the 64-task blocks b, b + G, ... (a dequeue atomic per block
@@ -3151,6 +3212,7 @@ __device__ __forceinline__ void defer_shadows_q(const KArgs& A, float4* slab) {
 template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     if constexpr (GEOM == 3 && TRT_SHADOW_REFILL && !TRT_BVH_COMPRESS && TRT_BVH_QUANT && TRT_BVH_WIDTH == 4) {
         if (A.bvh4 && A.bvh4q && A.nbatch != 0) {
             defer_shadows_q(A, slab);
@@ -3239,6 +3301,7 @@ template <int CAP, int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP, GEOM, false>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     Cnt cnt;
     const uint32_t n = A.dctr->nfb;
     const f3 orig = mk(A.fr[0].cam[0], A.fr[0].cam[1], A.fr[0].cam[2]);
@@ -3363,6 +3426,7 @@ __device__ __forceinline__ uint2 lv_level_range(const KArgs& A, uint32_t lvl) {
 template <int GEOM>
 __global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level0(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     const uint32_t tile = xcd_tile(A, blockIdx.x), lane = lane_id();
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
@@ -3379,6 +3443,7 @@ __global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level0(KArgs A) {
 template <int GEOM>
 __global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     const uint32_t lvl = A.lv_level;
     const uint2 nb = lv_level_range(A, lvl);
     const uint32_t n = nb.x, base = nb.y; // written entries, first event slot of this level
@@ -3451,6 +3516,7 @@ __device__ __forceinline__ void lvb_segment(const KArgs& A, bool valid, Seg cur,
 template <int GEOM>
 __global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level0(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     const uint32_t tile = xcd_tile(A, blockIdx.x), lane = lane_id();
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
@@ -3467,6 +3533,7 @@ __global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level0(KArgs A) {
 template <int GEOM>
 __global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     const uint32_t lvl = A.lv_level;
     const uint2 nb = lv_level_range(A, lvl);
     const uint32_t n = nb.x, base = nb.y;
@@ -3615,6 +3682,7 @@ template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void shadow_batch_kernel(KArgs A, const float4* __restrict__ rays,
                                                                                 uint32_t n, uint32_t* __restrict__ occ) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
+    top_fill<GEOM>(A, slab);
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n) return;
     const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];

@@ -676,6 +676,7 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // GEOM 3 kernels walk only the quantized nodes (trt_kernel.hip g3_quant_only): a scene whose
     // nodes did not quantize (or whose 4-wide stack would not fit) takes the GEOM 2 kernels.
     A.bvh_waves4 = c->d_bvh4q ? (c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : 1u) : 0u;
+    A.bvh4q_n = c->d_bvh4q ? (uint32_t)(c->scene_bytes[trt::kSceneBvh4Q] / sizeof(trt::Bvh4QNode)) : 0u;
     A.xcd_rot = c->xcd_rot;
     A.xcd_skew = c->xcd_skew;
     A.xcd_inter = c->xcd_inter;
