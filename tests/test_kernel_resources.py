@@ -1,0 +1,53 @@
+"""Register / scratch budgets of the hot kernels, read from the built gfx950 code object
+(tools/kres.py: the AMDGPU metadata of build/csrc/trt_kernel.o, no GPU needed).  A change that
+makes the 96-VGPR (5-wave) kernels spill much more shows up here before it costs a GPU run:
+the C2 kernel has no scratch at all, the C4 kernel stays near its measured spill level."""
+from __future__ import annotations
+
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+OBJ = REPO / "build" / "csrc" / "trt_kernel.o"
+
+
+@pytest.fixture(scope="module")
+def resources():
+    if not OBJ.exists():
+        pytest.skip("build/csrc/trt_kernel.o not built")
+    out = subprocess.run([sys.executable, str(REPO / "tools" / "kres.py"), "trace_kernel"], check=True,
+                         capture_output=True, text=True).stdout
+    res = {}
+    for line in out.splitlines():
+        m = re.match(r"void trt::trace_kernel<([^>]*)>\(trt::KArgs\)\s+vgpr\s+(\d+)\s+sgpr\s+(\d+)\s+scratch\s+(\d+)\s+lds\s+(\d+)",
+                     line)
+        if m:
+            res[m.group(1)] = dict(vgpr=int(m.group(2)), sgpr=int(m.group(3)), scratch=int(m.group(4)),
+                                   lds=int(m.group(5)))
+    assert res, out[:500]
+    return res
+
+
+def test_c2_kernel_has_no_scratch(resources):
+    """The headline kernel (C2: depth 4, no triangles, plain launches): 5 waves, no spills."""
+    r = resources["3, false, 0, false, false, false"]
+    assert r["vgpr"] <= 96 and r["scratch"] == 0, r
+
+
+def test_c4_kernel_scratch_budget(resources):
+    """C4 (depth 4, quantized BVH4): 96 VGPRs, the private segment stack (96 B) and the
+    traversal stack tail (192 B) plus the measured spill slots (432 B in round 5)."""
+    r = resources["3, false, 3, false, false, false"]
+    assert r["vgpr"] <= 96 and r["scratch"] <= 448, r
+
+
+def test_lds_fits_the_wave_targets(resources):
+    """LDS per one-wave workgroup times the waves per CU the launch bounds ask for stays within
+    the 160 KB of a gfx950 CU for the plain and deferred kernels."""
+    for key, waves in (("3, false, 0, false, false, false", 20), ("3, false, 3, false, false, false", 20),
+                       ("0, false, 3, false, true, false", 16)):
+        assert resources[key]["lds"] * waves <= 160 * 1024, (key, resources[key])

@@ -36,6 +36,8 @@ for v in "$@"; do
         cur) variant cur ;;
         late0) variant late0 -DTRT_LATE_MAT=0 ;;
         top21) variant top21 -DTRT_TOP_LDS=21 ;;
+        hotd1) variant hotd1 -DTRT_HOT_DIAG=1 ;;
+        hotd2) variant hotd2 -DTRT_HOT_DIAG=2 ;;
         top5) variant top5 -DTRT_TOP_LDS=5 ;;
         sh4late) variant sh4late -DTRT_G3_WAVES_SHALLOW=4 ;;
         g3p24) variant g3p24 -DTRT_G3_SEG_PRIV=1 -DTRT_G3_LDS=24 ;;

@@ -82,6 +82,7 @@ struct trt_ctx {
     uint32_t defer_sub = 0;
     uint32_t cur_in_flight = 1; // frames in flight of the current render call
     bool spp_lanes = true;      // spp > 1 frames: one lane per sample (TRT_SPP_LANES)
+    bool hot_first = false;     // single-frame plain launches deal last frame's costliest tiles first (TRT_HOT_FIRST)
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.
@@ -110,6 +111,14 @@ struct trt_ctx {
         trt::LevCtr* lv_ctr = nullptr;
         uint32_t* lv_flag = nullptr;
         size_t lv_evcap = 0, lv_qcap = 0, lv_npx = 0;
+        // Hot-first dealing state of single-frame plain launches (KArgs::hot): three lists of
+        // (count, longest wave, hot_max tiles) and three per-tile flag arrays, the tiling they
+        // index, the rotation counter, and the stream that owns them (only frames on that
+        // stream use them: stream order sequences their reads and writes).
+        uint32_t* hot = nullptr;
+        uint8_t* hot_flag = nullptr;
+        uint32_t hot_max = 0, hot_tiles = 0, hot_cap = 0, hot_k = 0;
+        hipStream_t hot_stream = nullptr;
         bool last_levels = false; // the slot's last deferred frame ran TRT_DEFER_LEVELS
         size_t last_npx = 0;
         // The stream of the slot's last frame and an event after it: a frame on another

@@ -292,6 +292,14 @@ struct KArgs {
     uint32_t* __restrict__ spilled;   // output pixels finished by finalize_spilled
     float4* __restrict__ diag;        // diagnostic builds only (TRT_DIAG_DUMP_SHADOW): ray dump
     uint32_t* __restrict__ persist;   // TRT_PERSIST builds: per-XCD tile tickets of this slot
+    // Hot-first dealing of single-frame plain launches (trace_hot): blocks [0, hot_max) trace
+    // the tiles the slot's previous frame found costliest, the others the remaining tiles in
+    // xcd_tile order.  hot: three lists of (count, longest wave duration, hot_max tiles), used
+    // in rotation (read hot_k % 3, write (hot_k + 1) % 3, clear (hot_k + 2) % 3); hot_flag: three
+    // per-tile flag arrays of hot_fstride bytes (1 = in that list).  hot_max = 0: off.
+    uint32_t* __restrict__ hot;
+    uint8_t* __restrict__ hot_flag;
+    uint32_t hot_max, hot_k, hot_fstride;
     // deferred shadows (defer != 0): event log, shadow query queue, per-pixel log heads
     uint32_t defer;
     uint32_t ev_cap;                  // event chunks per stripe (stripe s: chunks [s * ev_cap, ...))

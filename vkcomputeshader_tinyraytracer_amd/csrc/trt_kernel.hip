@@ -2849,6 +2849,61 @@ __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
     }
 }
 
+// Hot-first dealing (KArgs::hot, single-frame plain launches).  A single-frame launch ends with
+// its longest waves: in a C2 frame the costliest 8x8 tiles (glass-sphere pixels with 15-segment
+// trees and an envmap gather per miss) run 19-26 us against a 4.6 us median, and started at a
+// random point of the dispatch they leave the frame 30 us long against 13 us of total work /
+// slots (tools/waveclock.py, profiles/r05t_clock_c2_single_frame.log).  Neighbouring frames are
+// nearly the same, so each wave times its tile (s_memrealtime) and the tiles within 2x of the
+// previous frame's longest go into a list that the slot's next frame deals first (blocks
+// [0, hot_max)); the normal blocks skip the listed tiles.  Each tile is traced exactly once
+// either way, so the image does not depend on the lists (they only order the dispatch).
+#ifndef TRT_HOT_FIRST
+#define TRT_HOT_FIRST 1
+#endif
+// Block vb's tile, or ~0u when the block has nothing to trace (a spare hot block, or a tile a
+// hot block traces).  The block with vb == hot_max clears the list the slot's next frame writes.
+// TRT_HOT_DIAG (diagnostic builds): 1 = no recording (the lists stay empty), 2 = recording but
+// plain dealing (the lists are not read)
+#ifndef TRT_HOT_DIAG
+#define TRT_HOT_DIAG 0
+#endif
+__device__ __forceinline__ uint32_t hot_tile(const KArgs& A, uint32_t vb) {
+    const uint32_t L = A.hot_max + 2u, k = A.hot_k % 3u;
+    const uint32_t* rd = A.hot + k * L;
+    if (TRT_HOT_DIAG == 2) return vb < A.hot_max ? ~0u : xcd_tile(A, vb - A.hot_max);
+    if (vb < A.hot_max) return vb < min(rd[0], A.hot_max) ? rd[2u + vb] : ~0u;
+    if (vb == A.hot_max && lane_id() == 0u) {
+        uint32_t* z = A.hot + ((k + 2u) % 3u) * L;
+        z[0] = 0u;
+        z[1] = 0u;
+    }
+    const uint32_t tile = xcd_tile(A, vb - A.hot_max);
+    const uint8_t* rflag = A.hot_flag + (size_t)k * A.hot_fstride;
+    return (tile >= A.ntiles || rflag[tile]) ? ~0u : tile;
+}
+// After the tile: its wave's duration dt (10-ns ticks) against the previous frame's longest; a
+// tile within 2x of it goes into the list the slot's next frame deals first.
+__device__ __forceinline__ void hot_record(const KArgs& A, uint32_t tile, uint32_t dt) {
+    if (TRT_HOT_DIAG == 1 || lane_id() != 0u) return;
+    const uint32_t L = A.hot_max + 2u, k = A.hot_k % 3u, kw = (k + 1u) % 3u;
+    const uint32_t longest = A.hot[k * L + 1u];
+    uint32_t* wr = A.hot + kw * L;
+    // (the count is read first: once the list is full, no wave touches the contended counter)
+    bool hot = longest != 0u && 2u * dt >= longest &&
+               __hip_atomic_load(&wr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A.hot_max;
+    if (hot) {
+        const uint32_t s = __hip_atomic_fetch_add(&wr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s < A.hot_max) wr[2u + s] = tile;
+        else hot = false;
+    }
+    A.hot_flag[(size_t)kw * A.hot_fstride + tile] = hot ? 1u : 0u;
+    // the frame's longest wave: one contended address, so only a wave longer than the value it
+    // reads updates it (a per-wave atomic max on it cost 4x the frame)
+    if (dt > __hip_atomic_load(&wr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_fetch_max(&wr[1], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int GEOM, int TOP = top_nodes<GEOM>()>
 constexpr int slab_float4s() {
     return GEOM == 1 ? 64 * 3
@@ -2962,6 +3017,7 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
     // frame f = vb / ntiles of a multi-frame launch (plain frames only: split / deferred frames
     // and counting passes launch one frame)
     uint32_t f = 0, t = vb, tile;
+    bool hot = false; // wave-uniform: this block was dealt by hot_tile
     if (!SPLIT && !DEFER && A.spp_lanes) { // one lane per sample: ntiles * spp waves per frame
         const uint32_t per = A.ntiles * A.spp;
         f = vb / per;
@@ -2997,10 +3053,32 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
         tile = xcd_tile(A, t / A.defer_sub);
         trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % A.defer_sub);
         return;
+    } else if (!COUNT && !SPLIT && !DEFER && TRT_HOT_FIRST && TRT_WPB == 1 && A.hot_max) {
+        // hot-first dealing (one trace_tile call site with the plain path: a second inlined
+        // copy spilled the 96-VGPR kernels)
+        tile = __builtin_amdgcn_readfirstlane(hot_tile(A, vb)); // wave-uniform: keep it scalar
+        if (tile == ~0u) return;
+        hot = true;
     } else {
         tile = xcd_tile(A, t);
     }
+#if TRT_WPB == 1
+    // The tile and the start time wait in LDS (volatile: read back, not kept in registers) —
+    // values held across trace_tile cost the 96-VGPR kernels spills (SGPR spills live in VGPR
+    // lanes).  `hot` itself is re-read from the block index.
+    __shared__ volatile uint32_t hot_rec[2];
+    if (hot) {
+        hot_rec[0] = tile;
+        hot_rec[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
+#endif
     trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab);
+#if TRT_WPB == 1
+    if (!COUNT && !SPLIT && !DEFER && TRT_HOT_FIRST && A.hot_max && A.nframes <= 1u && !A.spp_lanes) {
+        const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        hot_record(A, hot_rec[0], t1 - hot_rec[1]);
+    }
+#endif
 #endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
@@ -3795,7 +3873,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
                                  ? (A.nframes + 1u) / 2u
                                  : std::max(A.nframes, 1u);
 #if TRT_WPB == 1
-    const dim3 fgrid(A.ntiles * fblocks);
+    // hot-first dealing (trace_hot): hot_max extra blocks ahead of the frame's tiles
+    const dim3 fgrid(A.ntiles * fblocks + (!count && TRT_HOT_FIRST && fblocks == 1u && A.nframes <= 1u && !A.spp_lanes ? A.hot_max : 0u));
 #else // TRT_WPB waves per workgroup: virtual blocks as in trace_kernel, whole groups of 8 blocks
     const dim3 fgrid(((A.ntiles * fblocks + 8 * TRT_WPB - 1) / (8 * TRT_WPB)) * 8);
 #endif

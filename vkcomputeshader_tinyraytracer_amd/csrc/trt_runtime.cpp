@@ -226,6 +226,7 @@ int trt_create(trt_ctx** out, int hip_device) {
         c->defer_design = std::strcmp(e, "levels") == 0 ? TRT_DEFER_LEVELS
                           : std::strcmp(e, "levels_b") == 0 ? TRT_DEFER_LEVELS_B : TRT_DEFER_POOL;
     if (const char* e = std::getenv("TRT_SPP_LANES")) c->spp_lanes = std::atoi(e) != 0;
+    if (const char* e = std::getenv("TRT_HOT_FIRST")) c->hot_first = std::atoi(e) != 0;
     if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32 or 16
         const int ppw = std::atoi(e);
         c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
@@ -245,6 +246,9 @@ int trt_destroy(trt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+    // frames of earlier trt_render calls may still run on other streams (render_slot): every
+    // buffer below may be in use until the device drains
+    (void)hipDeviceSynchronize();
     free_scene(c);
     (void)hipFree(c->d_envp);
     (void)hipFree(c->d_out8);
@@ -266,6 +270,8 @@ int trt_destroy(trt_ctx* c) {
         (void)hipFree(b.px_ev);
         (void)hipFree(b.fb);
         (void)hipFree(b.dctr);
+        (void)hipFree(b.hot);
+        (void)hipFree(b.hot_flag);
         if (b.done) (void)hipEventDestroy(b.done);
     }
     for (hipStream_t s : c->aux) {
@@ -981,6 +987,56 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     return TRT_OK;
 }
 
+// Hot-first dealing (trt_kernel.hip trace_hot) for a single-frame plain launch on `slot`: the
+// slot's lists (allocated, or cleared when the tiling changed) and the rotation step.  The
+// lists belong to the stream of the slot's first such frame; a frame on another stream deals
+// plainly and leaves them alone, so every read and write of them is ordered by that one stream
+// (no cross-stream waits).  Other launches get hot_max = 0.
+int prepare_hot(trt_ctx* c, KArgs& A, uint32_t slot, hipStream_t stream, bool count) {
+    A.hot = nullptr;
+    A.hot_flag = nullptr;
+    A.hot_max = A.hot_k = A.hot_fstride = 0;
+    if (!c->hot_first || count || A.split_w || A.defer || A.nframes > 1u || A.spp_lanes || A.ntiles < 64u) return TRT_OK;
+    auto& b = c->split[slot];
+    if (b.hot && b.hot_stream != stream) return TRT_OK;
+    static const uint32_t cap = [] {
+        const char* e = std::getenv("TRT_HOT_MAX");
+        return e ? std::max<uint32_t>(1u, (uint32_t)std::strtoul(e, nullptr, 10)) : 512u;
+    }();
+    const uint32_t hmax = std::max<uint32_t>(1u, std::min<uint32_t>(cap, A.ntiles / 16u));
+    if (!b.hot || A.ntiles > b.hot_cap || hmax != b.hot_max) {
+        if (b.hot) HIP_TRY(c, hipStreamSynchronize(b.hot_stream)); // its frames read the old lists
+        (void)hipFree(b.hot);
+        (void)hipFree(b.hot_flag);
+        b.hot = nullptr;
+        b.hot_flag = nullptr;
+        b.hot_cap = b.hot_tiles = 0;
+        hipError_t e = hipMalloc((void**)&b.hot, 3 * (size_t)(hmax + 2u) * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&b.hot_flag, 3 * (size_t)A.ntiles);
+        if (e != hipSuccess) {
+            (void)hipFree(b.hot);
+            b.hot = nullptr;
+            return hip_fail(c, e, "alloc hot-first lists");
+        }
+        b.hot_cap = A.ntiles;
+        b.hot_max = hmax;
+        b.hot_stream = stream;
+    }
+    if (b.hot_tiles != A.ntiles) { // another tiling: the lists index other tiles
+        HIP_TRY(c, hipMemsetAsync(b.hot, 0, 3 * (size_t)(b.hot_max + 2u) * sizeof(uint32_t), stream));
+        HIP_TRY(c, hipMemsetAsync(b.hot_flag, 0, 3 * (size_t)b.hot_cap, stream));
+        b.hot_tiles = A.ntiles;
+        b.hot_k = 0;
+    }
+    A.hot = b.hot;
+    A.hot_flag = b.hot_flag;
+    A.hot_max = b.hot_max;
+    A.hot_fstride = b.hot_cap;
+    A.hot_k = b.hot_k;
+    b.hot_k = (b.hot_k + 1u) % 3u;
+    return TRT_OK;
+}
+
 // After a split frame's launches on `stream`: the slot's fence.
 int fence_split(trt_ctx* c, const KArgs& A, uint32_t slot, hipStream_t stream) {
     if (!A.split_w && !A.defer) return TRT_OK;
@@ -1107,6 +1163,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
             if ((rc = prepare_split(c, p, A, slot, sv[slot])) != TRT_OK) return rc;
         }
         hipStream_t st = sv[slot];
+        if ((rc = prepare_hot(c, A, slot, st, false)) != TRT_OK) return rc;
         const bool timed = timing && j % every == 0;
         const size_t k = 2 * (size_t)(j / every);
         if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], st));
@@ -1213,6 +1270,7 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     const uint32_t slot = render_slot(c, c->stream);
     c->cur_in_flight = 1u; // one frame: its latency is the rate
     if ((rc = prepare_split(c, p, A, slot, c->stream)) != TRT_OK) return rc;
+    if ((rc = prepare_hot(c, A, slot, c->stream, count)) != TRT_OK) return rc;
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 32 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
@@ -1391,6 +1449,22 @@ extern "C" int trt_diag_defer_pad(trt_ctx* c, uint32_t slot, uint32_t* out16) {
     if (!c || !out16 || slot >= TRT_BUILD_MAX_IN_FLIGHT || !c->split[slot].dctr) return TRT_ERR_INVALID;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(out16, c->split[slot].dctr, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return TRT_OK;
+}
+
+// diagnostic: slot `slot`'s hot-first lists (trt_kernel.hip trace_hot): out[0..5] = (count,
+// longest wave in 10-ns ticks) of lists 0..2, out[6] = the list the slot's next frame reads,
+// out[7] = hot_max (0: the slot has run no hot-first frame).
+extern "C" int trt_diag_hot(trt_ctx* c, uint32_t slot, uint32_t* out8) {
+    if (!c || !out8 || slot >= TRT_BUILD_MAX_IN_FLIGHT) return TRT_ERR_INVALID;
+    const auto& b = c->split[slot];
+    std::memset(out8, 0, 8 * sizeof(uint32_t));
+    if (!b.hot) return TRT_OK;
+    HIP_TRY(c, hipDeviceSynchronize());
+    for (uint32_t l = 0; l < 3; ++l)
+        HIP_TRY(c, hipMemcpy(out8 + 2 * l, b.hot + (size_t)l * (b.hot_max + 2u), 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    out8[6] = b.hot_k;
+    out8[7] = b.hot_max;
     return TRT_OK;
 }
 
