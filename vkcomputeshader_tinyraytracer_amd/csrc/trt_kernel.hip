@@ -2858,6 +2858,12 @@ __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
 // previous frame's longest go into a list that the slot's next frame deals first (blocks
 // [0, hot_max)); the normal blocks skip the listed tiles.  Each tile is traced exactly once
 // either way, so the image does not depend on the lists (they only order the dispatch).
+// Measured and rejected (round 5, profiles/r05u_ab_hot_first.jsonl, r05x_ab_hot_first_*.jsonl):
+// with the lists dealt, a C2 frame at one launch per frame takes 100-120 us instead of 31 (2 in
+// flight: 72 vs 16 us), whatever the list length (8, 32, 128 or 512 tiles); recording alone
+// (lists written, not dealt) and dealing alone (extra blocks, plain order) cost 2-3 %.  The
+// runtime switch (trt_ctx::hot_first, TRT_HOT_FIRST=1) is off by default; this macro compiles
+// the path in for the tests (tests/test_gpu_hot.py: bit-identical frames).
 #ifndef TRT_HOT_FIRST
 #define TRT_HOT_FIRST 1
 #endif
