@@ -37,6 +37,9 @@ for v in "$@"; do
         late0) variant late0 -DTRT_LATE_MAT=0 ;;
         top21) variant top21 -DTRT_TOP_LDS=21 ;;
         hotd1) variant hotd1 -DTRT_HOT_DIAG=1 ;;
+        sub16) variant sub16 -DTRT_SHADOW_SUBSET=16 ;;
+        sub32) variant sub32 -DTRT_SHADOW_SUBSET=32 ;;
+        sub8) variant sub8 -DTRT_SHADOW_SUBSET=8 ;;
         hotd2) variant hotd2 -DTRT_HOT_DIAG=2 ;;
         top5) variant top5 -DTRT_TOP_LDS=5 ;;
         sh4late) variant sh4late -DTRT_G3_WAVES_SHALLOW=4 ;;

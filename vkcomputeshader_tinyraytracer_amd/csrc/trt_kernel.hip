@@ -1173,6 +1173,14 @@ __device__ __forceinline__ bool ray_misses_all_batches(f3 o, f3 d) {
 #ifndef TRT_SHADOW_WAVE_EXT
 #define TRT_SHADOW_WAVE_EXT 0.1
 #endif
+// TRT_SHADOW_SUBSET (min lanes, 0 = off): a wave whose shadow origins are not all near its first
+// lane's lets the near ones walk together (shadow_wave_q) and the rest alone.  Measured and
+// rejected (round 5, profiles/r05ac_ab_shadow_subset.jsonl): 8 / 16 / 32 lanes: C4 +12 / +10 /
+// +7 %, the shipped frame +16 / +11 / +5 % at 16 in flight — the two phases run one after the
+// other, and the lone walks are hardly shorter for having fewer lanes.
+#ifndef TRT_SHADOW_SUBSET
+#define TRT_SHADOW_SUBSET 0
+#endif
 constexpr int kShadowWaveStack = 128; // >= kBvhStack
 __device__ __forceinline__ bool shadow_wave_q(const KArgs& A, f3 o, f3 d, f3 inv, float max_dist, float4* slab) {
     typedef __attribute__((address_space(4))) const float cfloat;
@@ -1361,7 +1369,12 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
                 const float fy = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(o.y)));
                 const float fz = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(o.z)));
                 const float e = fmaxf(fmaxf(fabsf(o.x - fx), fabsf(o.y - fy)), fabsf(o.z - fz));
-                if (__ballot(!(e <= (float)TRT_SHADOW_WAVE_EXT)) == 0ull)
+                const bool near = e <= (float)TRT_SHADOW_WAVE_EXT;
+                const uint64_t nm = __ballot(near);
+                if (nm == __ballot(true)) return shadow_wave_q(A, o, d, inv, max_dist, slab);
+                // TRT_SHADOW_SUBSET: when at least that many lanes lie near the first one, those
+                // lanes walk together and only the others walk alone
+                if (TRT_SHADOW_SUBSET > 0 && __popcll(nm) >= (uint32_t)TRT_SHADOW_SUBSET && near)
                     return shadow_wave_q(A, o, d, inv, max_dist, slab);
             }
 #endif
