@@ -36,6 +36,7 @@ import hashlib
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -79,7 +80,7 @@ def parse():
     ap.add_argument("--extra-frames", type=int, default=160,
                     help="frames of the shipped / README-scene legs (16 run in flight: 160 keeps the pipeline's "
                          "fill and drain to a few per cent); 0 skips them")
-    ap.add_argument("--legs", default="c3,c5,c2pf",
+    ap.add_argument("--legs", default="c3,c5,c2pf,cabi",
                     help="extra legs (comma list; '' = none): c3 = BASELINE configs[2] (1920x1080 mesh), c5 = "
                          "configs[4] (4K, 16 spp), c2pf = C2 at one launch per frame, 2 in flight (drawFrame)")
     ap.add_argument("--legs-frames", type=int, default=200, help="frames of the C3 and per-frame-launch C2 legs")
@@ -709,6 +710,34 @@ def attach_traffic(rl: dict, td: dict | None) -> None:
     rl["traffic_detail"] = td
 
 
+# ---- the shipped frame through the C++ host at the reference host's defaults -----------------
+
+DROPIN_HOST = REPO / "tests" / "native" / "drop_in_host"
+DROPIN_DUMP = REPO / "tests" / "golden" / "dropin_meshes.bin"
+
+
+def c_abi_leg(frames: int) -> dict:
+    """The shipped frame (depth 20) through the C-ABI from a plain C++ process
+    (tests/native/drop_in_host --bench: the INTEGRATION.md §2 binding, no Python in the process),
+    once with the environment the reference's own host would start with — GPU_MAX_HW_QUEUES
+    unset, i.e. HIP's default of 4 hardware queues, the library's automatic in-flight count — and
+    once with 32 queues (what the Python package and this bench export)."""
+    out = {"note": "tests/native/drop_in_host --bench: trt_render_frames of the camera walk (auto in-flight "
+                   "count) and trt_render per frame into host memory (drawFrame pacing)"}
+    for key, queues in (("default_env", None), ("queues_32", "32")):
+        env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "LD_LIBRARY_PATH")}
+        if queues:
+            env["GPU_MAX_HW_QUEUES"] = queues
+        r = subprocess.run([str(DROPIN_HOST), "--bench", str(DROPIN_DUMP), str(frames)], capture_output=True,
+                           text=True, timeout=600, env=env)
+        if r.returncode != 0:
+            out[key] = {"error": r.stderr[-500:]}
+            continue
+        line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and "bench" in x][-1]
+        out[key] = {k: line[k] for k in ("gpu_max_hw_queues", "ms_per_frame", "fps", "draw_frame_ms", "frames")}
+    return out
+
+
 # ---- the BASELINE configs[2] / configs[4] legs and the drawFrame-paced C2 leg -----------------
 
 def config_leg(dev: int, name: str, frames: int, args, period: int) -> dict:
@@ -856,7 +885,7 @@ def main():
 
     legs = [x for x in args.legs.split(",") if x] if (rank == 0 and not dist_mode) else []
     for leg in legs:
-        key = {"c3": "c3_frame", "c5": "c5_frame", "c2pf": "c2_per_frame_launch"}.get(leg)
+        key = {"c3": "c3_frame", "c5": "c5_frame", "c2pf": "c2_per_frame_launch", "cabi": "shipped_frame_c_abi"}.get(leg)
         if key is None:
             continue
         try:
@@ -864,6 +893,8 @@ def main():
                 extras[key] = config_leg(dev, "C3", args.legs_frames, args, min(args.camera_period, 64))
             elif leg == "c5":
                 extras[key] = config_leg(dev, "C5", args.c5_frames, args, max(1, args.c5_frames))
+            elif leg == "cabi":
+                extras[key] = c_abi_leg(args.extra_frames)
             else:
                 extras[key] = c2_per_frame_leg(dev, args.legs_frames, args)
         except Exception as e:  # N = 1: report the failure in the line

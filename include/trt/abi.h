@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define TRT_ABI_VERSION 3
+#define TRT_ABI_VERSION 4
 
 /* status codes */
 #define TRT_OK 0
@@ -214,26 +214,10 @@ int trt_set_subtree_split(trt_ctx* ctx, int window);
 #define TRT_DEFER_ON 2
 int trt_set_deferred_shadows(trt_ctx* ctx, int mode);
 
-/* How a deferred frame is traced (all are bit-identical to the per-pixel loop):
- * TRT_DEFER_POOL (the default): passes A/B/C as described above, a tile's lanes sharing its
- * pending segments through an LDS pool.  TRT_DEFER_LEVELS (round 5, measured slower on the
- * shipped frame): breadth first, one launch per tree depth over the whole frame's
- * segments of that depth, each lane tracing one segment with its three shadow rays inline and
- * writing a 20-byte event (colour term + child slots); pass C sums each pixel's event tree in the
- * reference's pop order.  TRT_DEFER_LEVELS_B: the same levels without the shadow rays, which go
- * to the dense pass B with the pool design's events.  Also settable at context creation with
- * TRT_DEFER_MODE=pool|levels|levels_b. */
-#define TRT_DEFER_POOL 0
-#define TRT_DEFER_LEVELS 1
-#define TRT_DEFER_LEVELS_B 2
-int trt_set_defer_design(trt_ctx* ctx, int design);
-
 /* Counters of the last deferred frame rendered on `slot` (0 .. TRT_MAX_FRAMES_IN_FLIGHT-1;
- * trt_render uses one slot per stream).  TRT_DEFER_POOL / _LEVELS_B: out[0] event chunks taken,
- * out[1] shadow queries appended, out[2] pixels re-traced in place, out[3] chunk capacity, out[4]
- * query capacity.  TRT_DEFER_LEVELS: out[0] events written, out[1] entries of the largest level queue,
- * out[2] pixels re-traced in place, out[3] event capacity, out[4] entries per level queue.
- * Waits for the context's stream. */
+ * trt_render uses one slot per stream): out[0] event chunks taken, out[1] shadow queries
+ * appended, out[2] pixels re-traced in place, out[3] chunk capacity, out[4] query capacity (of
+ * the slot's allocation).  Waits for the context's stream. */
 int trt_defer_stats(trt_ctx* ctx, uint32_t slot, uint64_t out[5]);
 
 /* The reference's frame loop (mainLoop -> drawFrame, main.cpp:405-438, 2181-2205) in one

@@ -8,6 +8,14 @@
 //   drop_in_host <mesh_dump> <out_dir>     render the frames below; one raw RGBA8 file per frame
 //                                          (<out_dir>/<name>.rgba) and one JSON line per frame
 //   drop_in_host --envmap W H <out_file>   write the synthetic envmap (no GPU; checks the port)
+//   drop_in_host --bench <mesh_dump> <frames> [in_flight]
+//                                          time the shipped frame along the camera walk through
+//                                          the C-ABI with this process's environment (bench.py
+//                                          runs it with GPU_MAX_HW_QUEUES unset, as the reference's
+//                                          own host would start): `frames` frames in one
+//                                          trt_render_frames call (auto in-flight count, or
+//                                          `in_flight`), then the drawFrame pacing (trt_render into
+//                                          host memory, one call per frame); one JSON line
 //
 // Frames (1024x768):
 //   shipped          the shipped frame: glass + whisky + ice (config.hpp:97-101) from the mesh
@@ -22,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -196,23 +205,8 @@ void print_runtime() {
                 rt, hip.c_str(), rccl.c_str(), trt_version());
 }
 
-} // namespace
-
-int main(int argc, char** argv) {
-    if (argc == 5 && std::string(argv[1]) == "--envmap") {
-        const uint32_t W = (uint32_t)std::strtoul(argv[2], nullptr, 10), H = (uint32_t)std::strtoul(argv[3], nullptr, 10);
-        const std::vector<uint8_t> env = synthetic_envmap(W, H);
-        FILE* f = std::fopen(argv[4], "wb");
-        if (!f || std::fwrite(env.data(), 1, env.size(), f) != env.size()) die("cannot write envmap");
-        std::fclose(f);
-        return 0;
-    }
-    if (argc != 3) die("usage: drop_in_host <mesh_dump> <out_dir> | --envmap W H <out_file>");
-    const std::vector<Mesh> meshes = read_dump(argv[1]);
-    const std::string out_dir = argv[2];
-    const std::vector<uint8_t> env = synthetic_envmap(7616, 3808);
-
-    // createShaderStorageBuffers (main.cpp:1494): the modelList loop through the C-ABI builder
+// The shipped scene (config.hpp:97-101) from the mesh dump through the C-ABI builder, uploaded.
+void upload_shipped(trt_ctx* ctx, const std::vector<Mesh>& meshes, const std::vector<uint8_t>& env, const trt_ubo& ubo) {
     trt_scene* sb = nullptr;
     check(trt_scene_create(&sb), "trt_scene_create");
     for (const ModelInfo& mi : MODEL_LIST) {
@@ -227,15 +221,86 @@ int main(int argc, char** argv) {
     }
     std::printf("{\"scene_triangles\": %u, \"scene_batches\": %u}\n", trt_scene_triangle_count(sb),
                 trt_scene_model_count(sb));
-
-    trt_ctx* ctx = nullptr;
-    check(trt_create(&ctx, 0), "trt_create");
-    print_runtime();
-    const trt_ubo ubo = make_ubo(0, 0, 0);
     check(trt_upload_scene(ctx, &ubo, trt_scene_triangles(sb), trt_scene_triangle_count(sb), trt_scene_models(sb),
                            trt_scene_model_count(sb), env.data(), 7616, 3808),
           "trt_upload_scene", ctx);
     trt_scene_destroy(sb);
+}
+
+// --bench: the shipped frame's rate through the C-ABI as a C++ host with its own environment.
+int bench(const std::vector<Mesh>& meshes, uint32_t frames, uint32_t in_flight) {
+    const std::vector<uint8_t> env = synthetic_envmap(7616, 3808);
+    trt_ctx* ctx = nullptr;
+    check(trt_create(&ctx, 0), "trt_create");
+    const trt_ubo ubo = make_ubo(0, 0, 0);
+    upload_shipped(ctx, meshes, env, ubo);
+    check(trt_set_frames_in_flight(ctx, in_flight), "trt_set_frames_in_flight", ctx);
+    trt_params rp;
+    trt_params_default(&rp); // 1024x768, depth 20, reference flags
+    const size_t fb = (size_t)rp.width * rp.height * 4;
+    const uint32_t nbuf = 16; // distinct images for concurrent frames
+    uint8_t* dev = nullptr;
+    hcheck(hipMalloc(reinterpret_cast<void**>(&dev), nbuf * fb), "hipMalloc");
+    trt_params p = rp;
+    p.flags |= TRT_FLAG_DEVICE_PTRS;
+    const std::vector<trt_ubo> walk = camera_walk(frames);
+    using clk = std::chrono::steady_clock;
+    auto run_loop = [&](uint32_t n) { // n frames of the walk, frame i into image i % nbuf
+        for (uint32_t i0 = 0; i0 < n; i0 += nbuf) {
+            const uint32_t k = std::min(nbuf, n - i0);
+            check(trt_render_frames(ctx, &p, walk.data() + i0, k, dev, fb, 0), "trt_render_frames", ctx);
+        }
+        check(trt_synchronize(ctx), "trt_synchronize", ctx);
+    };
+    run_loop(std::min(frames, 2 * nbuf)); // warmup: scratch, streams, clocks
+    const auto t0 = clk::now();
+    run_loop(frames);
+    const double loop_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    // drawFrame pacing: one trt_render per frame into host memory (the INTEGRATION.md binding)
+    std::vector<uint8_t> host(fb);
+    const uint32_t nd = std::min<uint32_t>(frames, 40);
+    for (uint32_t i = 0; i < 4; ++i) check(trt_render(ctx, &rp, host.data(), nullptr, nullptr), "trt_render", ctx);
+    const auto t1 = clk::now();
+    for (uint32_t i = 0; i < nd; ++i) {
+        check(trt_update_ubo(ctx, &walk[i]), "trt_update_ubo", ctx);
+        check(trt_render(ctx, &rp, host.data(), nullptr, nullptr), "trt_render", ctx);
+    }
+    const double draw_ms = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    std::printf("{\"bench\": \"shipped_frame_c_abi\", \"gpu_max_hw_queues\": \"%s\", \"in_flight_setting\": %u, "
+                "\"frames\": %u, \"ms_per_frame\": %.4f, \"fps\": %.1f, \"draw_frame_ms\": %.4f, "
+                "\"draw_frames\": %u}\n",
+                q ? q : "unset", in_flight, frames, loop_ms / frames, 1000.0 * frames / loop_ms, draw_ms / nd, nd);
+    hcheck(hipFree(dev), "hipFree");
+    check(trt_destroy(ctx), "trt_destroy");
+    return 0;
+}
+
+} // namespace
+
+int main(int argc, char** argv) {
+    if ((argc == 4 || argc == 5) && std::string(argv[1]) == "--bench")
+        return bench(read_dump(argv[2]), (uint32_t)std::strtoul(argv[3], nullptr, 10),
+                     argc == 5 ? (uint32_t)std::strtoul(argv[4], nullptr, 10) : 0u);
+    if (argc == 5 && std::string(argv[1]) == "--envmap") {
+        const uint32_t W = (uint32_t)std::strtoul(argv[2], nullptr, 10), H = (uint32_t)std::strtoul(argv[3], nullptr, 10);
+        const std::vector<uint8_t> env = synthetic_envmap(W, H);
+        FILE* f = std::fopen(argv[4], "wb");
+        if (!f || std::fwrite(env.data(), 1, env.size(), f) != env.size()) die("cannot write envmap");
+        std::fclose(f);
+        return 0;
+    }
+    if (argc != 3) die("usage: drop_in_host <mesh_dump> <out_dir> | --envmap W H <out_file>");
+    const std::vector<Mesh> meshes = read_dump(argv[1]);
+    const std::string out_dir = argv[2];
+    const std::vector<uint8_t> env = synthetic_envmap(7616, 3808);
+
+    // createShaderStorageBuffers (main.cpp:1494): the modelList loop through the C-ABI builder
+    trt_ctx* ctx = nullptr;
+    check(trt_create(&ctx, 0), "trt_create");
+    print_runtime();
+    const trt_ubo ubo = make_ubo(0, 0, 0);
+    upload_shipped(ctx, meshes, env, ubo);
 
     trt_params rp;
     trt_params_default(&rp); // 1024x768, depth 20, reference flags

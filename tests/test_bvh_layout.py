@@ -1,8 +1,9 @@
-"""The BVH pipeline of trt_upload_scene on the host (no GPU): the 4-wide collapse, the
-quantized nodes and their 48-byte form with implicit children (trt_device.h Bvh4CNode) build
-for every mesh configuration, and the compression's self-check passes — the kernel's own decode
-of every node (bvh4c_children, shared host/device) yields the remapped child references slot by
-slot and every leaf keeps its triangles.  The GPU parity tests then run the walk over them."""
+"""The BVH pipeline of trt_upload_scene on the host (no GPU): the 4-wide collapse and the
+quantized nodes build for every mesh configuration, the build is conservative (every point of
+every triangle lies inside the boxes of a root-to-leaf path of a leaf referencing it), and its
+depth stays within the traversal stack (kBvhStack = 64) even for centroid distributions that
+make binned SAH peel off one primitive per level.  The GPU parity tests then run the walk over
+them."""
 from __future__ import annotations
 
 import ctypes
@@ -23,11 +24,11 @@ def _build(sc):
     out = (ctypes.c_uint64 * 6)()
     rc = L.trt_diag_bvh_build(tris.ctypes.data, len(tris), models.ctypes.data, len(models), out)
     assert rc == 0
-    return dict(zip(("bvh2", "bvh4", "quantized", "compressed", "stack", "tris"), list(out)))
+    return dict(zip(("bvh2", "bvh4", "quantized", "depth", "stack", "tris"), list(out)))
 
 
 @pytest.mark.parametrize("name", ["C3", "C4", "ref", "readme"])
-def test_bvh4_compressed_layout(name, golden_meshes):
+def test_bvh4_layout(name, golden_meshes):
     if name == "ref":
         sc = S.config_reference_default(golden_meshes, env_size=(64, 32))
     elif name == "readme":
@@ -37,7 +38,7 @@ def test_bvh4_compressed_layout(name, golden_meshes):
     st = _build(sc)
     assert st["tris"] >= len(sc.tris)  # leaf references: spatial splits duplicate some
     assert 0 < st["bvh4"] < st["bvh2"] and st["stack"] <= 64
-    assert st["quantized"] == 1 and st["compressed"] == 1, st
+    assert st["quantized"] == 1 and 1 <= st["depth"] <= 64, st
 
 
 def _export(sc):
@@ -117,3 +118,35 @@ def test_every_triangle_point_is_inside_a_leaf_path(name, golden_meshes):
         inside = ((pts >= eff_lo[ri][:, None, :]) & (pts <= eff_hi[ri][:, None, :])).all(-1)
         covered |= inside & has[:, None]
     assert covered.all(), f"{int((~covered).sum())} triangle points outside every leaf path of their triangle"
+
+
+def _strip_scene(xs, w=1.0):
+    """One batch of small triangles at x = xs (y, z fixed), each w wide."""
+    n = len(xs)
+    tris = np.zeros(n, T.TRIANGLE)
+    for i, x in enumerate(xs):
+        tris[i]["v0"] = (x, 0.0, -10.0, 1.0)
+        tris[i]["v1"] = (x + w, 0.0, -10.0, 1.0)
+        tris[i]["v2"] = (x, w, -10.0, 1.0)
+    models = np.zeros(1, T.MODEL)
+    models[0]["params0"] = (0, n, 0, 0)
+    return tris, models
+
+
+@pytest.mark.parametrize("base,n", [(2.0, 120), (1.2, 400), (1.05, 1400), (None, 1400)])
+def test_bvh_depth_is_bounded(base, n):
+    """Advisor round 5 (high): binned SAH splits past kBvhSahDepth could peel a few primitives
+    per level (geometrically spaced centroids put all but the largest in the first bin), so the
+    BVH2 depth was unbounded while the BVH2 walk's stack holds kBvhStack = 64 entries — and these
+    scenes' BVH4 needs a stack deeper than 64 (out[4]), so the runtime does fall back to that walk.
+    The build now switches to median splits below that depth: depth <= 32 + log2(n) + 1."""
+    xs = [base ** k for k in range(n)] if base else list(np.linspace(-5.0, 5.0, n))
+    tris, models = _strip_scene(xs)
+    L = lib()
+    L.trt_diag_bvh_build.restype = ctypes.c_int
+    L.trt_diag_bvh_build.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    out = (ctypes.c_uint64 * 6)()
+    assert L.trt_diag_bvh_build(tris.ctypes.data, n, models.ctypes.data, 1, out) == 0
+    depth = int(out[3])
+    assert 1 <= depth <= 32 + int(np.ceil(np.log2(n))) + 1 <= 64, (base, depth, list(out))

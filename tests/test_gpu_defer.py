@@ -1,16 +1,13 @@
-"""GPU: deferred frames (trt_set_deferred_shadows), in every design (trt_set_defer_design):
-pool (default) — pass A traces every pixel's tree without shadow rays and logs its colour
-events, the tile's lanes sharing pending segments, pass B traces the frame's shadow queries
-densely — levels — one launch per tree depth over the whole frame, shadow rays inline, 20-byte
-events — and levels_b — the same levels with pass B; in all, pass C sums each pixel's events in
-the reference's pop order.
+"""GPU: deferred frames (trt_set_deferred_shadows): pass A traces every pixel's tree without
+shadow rays and logs its colour events, the tile's lanes sharing pending segments, pass B traces
+the frame's shadow queries densely, and pass C sums each pixel's events in the reference's pop
+order.
 
 The bar is bitwise: a deferred frame must equal the per-pixel loop without subtree split (the
 reference's single running sum, shader.comp:423-583) in both outputs, and — through it — the
 reference-order oracle within the usual RGBA8 / rayOut bar, at the shipped frame's full size.
 Pixels whose event log does not fit (tiny capacities forced through the test hooks
-TRT_DEFER_EVCAP / TRT_DEFER_QCAP, and TRT_LV_EVCAP / TRT_LV_QCAP for the level design) are
-re-traced in place and must not change a bit either."""
+TRT_DEFER_EVCAP / TRT_DEFER_QCAP) are re-traced in place and must not change a bit either."""
 from __future__ import annotations
 
 import numpy as np
@@ -26,18 +23,6 @@ pytestmark = pytest.mark.gpu
 
 SMALL_ENV = (1024, 512)
 DEFER_AUTO, DEFER_OFF, DEFER_ON = 0, 1, 2
-POOL, LEVELS, LEVELS_B = 0, 1, 2
-DEFAULT = POOL
-DESIGNS = {"pool": POOL, "levels": LEVELS, "levels_b": LEVELS_B}
-
-
-@pytest.fixture(params=["pool", "levels", "levels_b"])
-def design(request, gpu_renderer):
-    """Runs the test under each deferred-frame design; the default is restored after."""
-    gpu_renderer.set_defer_design(DESIGNS[request.param])
-    yield request.param
-    gpu_renderer.set_defer_design(DEFAULT)
-
 
 def _frame(r, sc, defer, split=1, p=None):
     r.set_deferred_shadows(defer)
@@ -69,7 +54,7 @@ def scenes(golden_meshes):
 
 
 @pytest.mark.parametrize("name", ["ref", "readme", "c3", "c2d12", "c1"])
-def test_deferred_frame_is_bit_identical_to_the_unsplit_loop(gpu_renderer, scenes, name, design):
+def test_deferred_frame_is_bit_identical_to_the_unsplit_loop(gpu_renderer, scenes, name):
     sc = scenes[name]
     gpu_renderer.upload_scene(sc)
     d8, d32 = _frame(gpu_renderer, sc, DEFER_ON)
@@ -84,20 +69,15 @@ def test_deferred_frame_is_bit_identical_to_the_unsplit_loop(gpu_renderer, scene
 @pytest.mark.parametrize("name", ["ref", "readme", "c3", "c2d12"])
 @pytest.mark.parametrize("window", [2, 3, 4, 5])
 def test_deferred_split_keeps_the_reference_order(gpu_renderer, scenes, name, window):
-    """Subtree split of a pool-design deferred frame: subtrees traced by other lanes log into
-    chains of their own, reached through LINK events at the place of their events: the image is
-    still the unsplit loop's bit for bit (no fixed-point sums).  (The level design does not
-    split: every launch already spreads one depth over the whole frame.)"""
-    gpu_renderer.set_defer_design(POOL)
+    """Subtree split of a deferred frame: subtrees traced by other lanes log into chains of
+    their own, reached through LINK events at the place of their events: the image is still the
+    unsplit loop's bit for bit (no fixed-point sums)."""
     sc = scenes[name]
     if window >= sc.max_depth:
         pytest.skip("window covers the whole tree: no split")
     gpu_renderer.upload_scene(sc)
-    try:
-        d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=window)
-        st = gpu_renderer.defer_stats(0)
-    finally:
-        gpu_renderer.set_defer_design(DEFAULT)
+    d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=window)
+    st = gpu_renderer.defer_stats(0)
     u8, u32 = _frame(gpu_renderer, sc, DEFER_OFF, split=1)
     assert st["fallback_pixels"] == 0, st
     assert np.array_equal(d8, u8) and np.array_equal(d32, u32)
@@ -109,19 +89,15 @@ def test_deferred_split_task_queue_overflow(gpu_renderer, scenes, monkeypatch):
     gpu_renderer.upload_scene(sc)
     u8, u32 = _frame(gpu_renderer, sc, DEFER_OFF, split=1)
     monkeypatch.setenv("TRT_SPLIT_QCAP", "64")
-    gpu_renderer.set_defer_design(POOL)
-    try:
-        d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=2)
-        st = gpu_renderer.defer_stats(0)
-    finally:
-        gpu_renderer.set_defer_design(DEFAULT)
+    d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=2)
+    st = gpu_renderer.defer_stats(0)
     monkeypatch.delenv("TRT_SPLIT_QCAP")
     assert st["fallback_pixels"] > 0, st
     assert np.array_equal(d8, u8) and np.array_equal(d32, u32)
 
 
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 7, 20])
-def test_deferred_depths(gpu_renderer, scenes, depth, design):
+def test_deferred_depths(gpu_renderer, scenes, depth):
     sc = scenes["c3"]
     gpu_renderer.upload_scene(sc)
     p = sc.params()
@@ -131,7 +107,7 @@ def test_deferred_depths(gpu_renderer, scenes, depth, design):
     assert np.array_equal(d8, u8) and np.array_equal(d32, u32)
 
 
-def test_shipped_frame_full_size_deferred_vs_reference_order_oracle(gpu_renderer, golden_meshes, design):
+def test_shipped_frame_full_size_deferred_vs_reference_order_oracle(gpu_renderer, golden_meshes):
     """The shipped frame (glass + water + ice, depth 20) at 1024x768 through the default
     (automatic) path — a deferred frame — against the oracle's reference-order running sum."""
     sc = S.config_reference_default(golden_meshes, env_size=SMALL_ENV)
@@ -144,32 +120,27 @@ def test_shipped_frame_full_size_deferred_vs_reference_order_oracle(gpu_renderer
     assert_float_close(g32, o32)
 
 
-@pytest.mark.parametrize("dsg,hook,value", [("pool", "TRT_DEFER_EVCAP", "8"), ("pool", "TRT_DEFER_QCAP", "300"),
-                                            ("pool", "TRT_DEFER_EVCAP", "0"), ("levels", "TRT_LV_EVCAP", "0"),
-                                            ("levels", "TRT_LV_EVCAP", "60000"), ("levels", "TRT_LV_QCAP", "500"),
-                                            ("levels", "TRT_LV_QCAP", "0"), ("levels_b", "TRT_LV_EVCAP", "60000"),
-                                            ("levels_b", "TRT_LV_QCAP", "500"), ("levels_b", "TRT_DEFER_QCAP", "300")])
-def test_overflow_pixels_are_retraced_in_place(gpu_renderer, scenes, monkeypatch, dsg, hook, value):
-    """Children that do not fit (event slots or a level queue; the pool design's event chunks or
-    query queue) send their pixels to the in-place fallback: the image must not change a bit.
-    TRT_LV_EVCAP=0 leaves only the primary rays' slots (every child overflows)."""
+@pytest.mark.parametrize("hook,value", [("TRT_DEFER_EVCAP", "8"), ("TRT_DEFER_QCAP", "300"), ("TRT_DEFER_EVCAP", "0")])
+def test_overflow_pixels_are_retraced_in_place(gpu_renderer, scenes, monkeypatch, hook, value):
+    """Children that do not fit (event chunks or the query queue) send their pixels to the
+    in-place fallback: the image must not change a bit.  TRT_DEFER_EVCAP=0 leaves no event slot
+    at all (every pixel is re-traced)."""
     sc = scenes["ref"]
     gpu_renderer.upload_scene(sc)
     u8, u32 = _frame(gpu_renderer, sc, DEFER_OFF)
     monkeypatch.setenv(hook, value)
-    gpu_renderer.set_defer_design(DESIGNS[dsg])
-    try:
-        for split in ((1, 3) if dsg == "pool" else (1,)):
-            d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=split)
-            st = gpu_renderer.defer_stats(0)
-            assert st["fallback_pixels"] > 0, (split, st)
-            assert np.array_equal(d8, u8) and np.array_equal(d32, u32), split
-    finally:
-        gpu_renderer.set_defer_design(DEFAULT)
+    for split in (1, 3):
+        d8, d32 = _frame(gpu_renderer, sc, DEFER_ON, split=split)
+        st = gpu_renderer.defer_stats(0)
+        assert st["fallback_pixels"] > 0, (split, st)
+        # the stats count against the capacity the frame ran with (the hook's), not the allocation
+        if hook == "TRT_DEFER_QCAP":
+            assert st["queries"] <= int(value) * 128, st
+        assert np.array_equal(d8, u8) and np.array_equal(d32, u32), split
     monkeypatch.delenv(hook)
 
 
-def test_deferred_frames_in_flight(gpu_renderer, scenes, design):
+def test_deferred_frames_in_flight(gpu_renderer, scenes):
     """render_frames with 1..4 frames in flight (one scratch set per slot): every frame equals
     the single deferred frame."""
     sc = scenes["ref"]
@@ -191,7 +162,7 @@ def test_deferred_frames_in_flight(gpu_renderer, scenes, design):
         gpu_renderer.set_deferred_shadows(DEFER_AUTO)
 
 
-def test_deferred_bands_and_ray_replay(gpu_renderer, scenes, design):
+def test_deferred_bands_and_ray_replay(gpu_renderer, scenes):
     """Band launches (the multi-GPU tiling's unit) and binding-1 ray replay go through the
     deferred passes unchanged."""
     sc = scenes["ref"]
@@ -216,7 +187,7 @@ def test_deferred_bands_and_ray_replay(gpu_renderer, scenes, design):
     assert np.array_equal(r8, full8)
 
 
-def test_batch_walk_deferred(gpu_renderer, scenes, design):
+def test_batch_walk_deferred(gpu_renderer, scenes):
     sc = scenes["ref"]
     gpu_renderer.upload_scene(sc)
     p = sc.params()
@@ -267,4 +238,34 @@ def test_pass_a_pixels_per_wave(scenes, ppw):
             assert np.array_equal(d8, u8) and np.array_equal(d32, u32), name
             assert r.defer_stats(0)["fallback_pixels"] == 0
     finally:
+        r.close()
+
+
+def test_auto_in_flight_drops_a_slot_that_runs_out_of_memory(scenes, monkeypatch):
+    """Auto frames in flight: a slot whose deferred scratch cannot be allocated (out of memory,
+    injected for slot 2 through the test hooks) is dropped with the slots after it, the failed
+    allocation's error does not leak into the next launch, and every frame still equals the
+    single deferred frame."""
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    sc = scenes["ref"]
+    r = trt.Renderer(0)
+    try:
+        r.upload_scene(sc)
+        u8, _ = _frame(r, sc, DEFER_OFF)
+        monkeypatch.setenv("TRT_ENABLE_TEST_HOOKS", "1")
+        monkeypatch.setenv("TRT_TEST_FAIL_DEFER_SLOT", "2")
+        p = sc.params()
+        out = torch.zeros((6, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+        r.set_deferred_shadows(DEFER_ON)
+        r.render_frames(p, out, 6, frame_stride=p.height * p.width * 4)
+        torch.cuda.synchronize()
+        for f in range(6):
+            assert np.array_equal(out[f].cpu().numpy(), u8), f
+        # an explicit in-flight count is the caller's: the same failure is reported, not hidden
+        r.set_frames_in_flight(4)
+        with pytest.raises(trt.TrtError):
+            r.render_frames(p, out, 6, frame_stride=p.height * p.width * 4)
+    finally:
+        monkeypatch.delenv("TRT_TEST_FAIL_DEFER_SLOT", raising=False)
         r.close()

@@ -77,3 +77,28 @@ def test_c5_16_spread_rows(gpu_renderer, index):
     for k in T.Stats.EXACT:
         assert gst[k] == ost[k], (k, gst[k], ost[k])
     assert_rgba8_close(g8, o8)
+
+
+def test_c4_whole_frame():
+    """Round-6 verdict item 6: one WHOLE C4 frame (3840x2160, 102,400 triangles, depth 4) — all
+    2,160 rows — against the oracle, exact ray / triangle / batch counters and the RGBA8 bar.
+    This replaces the kernel's own earlier frame hash as the only whole-frame C4 check (the
+    oracle takes ~1-2 minutes of the box's 16-CPU share for it)."""
+    import time
+
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    sc = S.CONFIGS["C4"]()
+    p = sc.params()
+    with trt.Renderer(0) as r:
+        r.upload_scene(sc)
+        g8, _, gst = r.draw_frame(p, count=True)
+        g8b, _, _ = r.draw_frame(p)  # the plain launch the bench times
+    t0 = time.time()
+    o8, _, ost = orc.render(sc, p, threads=0)
+    print(f"\noracle: whole C4 frame in {time.time() - t0:.1f} s")
+    assert g8.shape == o8.shape == (2160, 3840, 4)
+    for k in T.Stats.EXACT:
+        assert gst[k] == ost[k], (k, gst[k], ost[k])
+    assert_rgba8_close(g8, o8)
+    assert (g8b == g8).all()

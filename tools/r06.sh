@@ -1,0 +1,51 @@
+#!/usr/bin/env bash
+# Round-6 GPU runner: one script, one stage per argument (run on the box through gpurun), e.g.
+#   gpurun -- 'bash tools/r06.sh hotrepro prof'
+# Every GPU step has its own time limit; the script stops at the first failing step.
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${R06_TAG:-r06}"
+OUT="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
+cd "$ROOT"
+export GPU_MAX_HW_QUEUES=32
+PYT="python -u -m pytest -x -v --timeout 150 --timeout-method thread"
+
+step() { # step <name> <seconds> <command...>: runs, logs to $OUT/<name>.log, stops on failure
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  tail -4 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then echo "!! $name rc=$rc"; exit $rc; fi
+}
+
+for stage in "$@"; do
+  case $stage in
+  tests) # the whole GPU suite
+    TRT_PARITY_LOG="$OUT/parity_log.jsonl" step pytest_gpu 1000 $PYT -m gpu tests ;;
+  smoke)
+    step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+  bench) # the driver's command
+    step bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+  prof) # rocprofv3 kernel trace of the bench command, split per (kernel, grid)
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+      python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu --traffic off > "$OUT/prof_bench.log" 2>&1) \
+      || { tail -20 "$OUT/prof_bench.log"; exit 1; }
+    db=$(find "$OUT/prof" -name '*.db' | head -1)
+    python tools/rocpd_stats.py --split-grid "$db" "$OUT/kernel_stats_by_grid.csv"
+    python tools/rocpd_stats.py "$db" "$OUT/kernel_stats.csv"
+    grep '^{' "$OUT/prof_bench.log" | tail -1 > "$OUT/prof_bench_line.json"
+    rm -rf "$OUT/prof"
+    head -6 "$OUT/kernel_stats_by_grid.csv" | cut -c1-200 ;;
+  kbench) # kbench legs named in KB (e.g. KB="C2:--frame-batch 20;shipped:--inflight 16")
+    IFS=';' read -ra legs <<< "${KB:-}"
+    for leg in "${legs[@]}"; do
+      cfg=${leg%%:*}; args=${leg#*:}
+      step "kb_${cfg}" 300 python tools/kbench.py --config "$cfg" $args --tag "$leg"
+      grep '^{' "$OUT/kb_${cfg}.log" >> "$OUT/kb.jsonl"
+    done ;;
+  *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done

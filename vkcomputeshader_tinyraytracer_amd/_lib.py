@@ -75,7 +75,6 @@ def lib() -> ctypes.CDLL:
         "trt_set_frames_in_flight": (c_int, [vp, c_u32]),
         "trt_set_subtree_split": (c_int, [vp, c_int]),
         "trt_set_deferred_shadows": (c_int, [vp, c_int]),
-        "trt_set_defer_design": (c_int, [vp, c_int]),
         "trt_defer_stats": (c_int, [vp, c_u32, ctypes.POINTER(ctypes.c_uint64)]),
         "trt_render_frames": (c_int, [vp, ctypes.POINTER(Params), vp, c_u32, vp, ctypes.c_size_t, c_u32]),
         "trt_frame_times": (c_int, [vp, ctypes.POINTER(ctypes.c_float), c_u32]),
@@ -149,7 +148,6 @@ ABI_SYMBOLS = (
     "trt_set_frames_in_flight",
     "trt_set_subtree_split",
     "trt_set_deferred_shadows",
-    "trt_set_defer_design",
     "trt_defer_stats",
     "trt_render_frames",
     "trt_frame_times",

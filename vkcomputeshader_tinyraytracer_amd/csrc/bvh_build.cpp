@@ -305,7 +305,7 @@ struct SplitBuilder {
         float best = std::numeric_limits<float>::infinity();
         int best_axis = -1, best_k = -1;
         Box best_l, best_r;
-        for (int a = 0; a < 3; ++a) {
+        for (int a = 0; a < 3 && depth < kBvhSahDepth; ++a) {
             const float ea = cb.hi[a] - cb.lo[a];
             if (!(ea > 0.0f)) continue;
             Box bins[NB];
@@ -350,6 +350,10 @@ struct SplitBuilder {
         float sbest = std::numeric_limits<float>::infinity();
         int s_axis = -1;
         double s_plane = 0.0;
+        // Past kBvhSahDepth only median splits (as Builder): a binned split can peel off one bin
+        // per level (geometrically spaced centroids), so without this the depth — and the BVH2
+        // walk's stack, kBvhStack entries — would be unbounded.  With it: <= 32 + log2(n) + 1.
+        if (depth >= kBvhSahDepth) best_axis = -1, best = std::numeric_limits<float>::infinity();
         bool try_spatial = depth < kBvhSahDepth && budget > 0;
         if (try_spatial && best_axis >= 0) {
             const Box ov = intersect(best_l, best_r);
@@ -494,6 +498,8 @@ Box tri_box(const trt_triangle& t) {
 
 } // namespace
 
+uint32_t bvh_depth(const std::vector<BvhNode>& b2);
+
 // Returns false (no BVH) when batch ranges overlap, a triangle is NaN, or nothing is covered.
 bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris) {
@@ -564,6 +570,10 @@ bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models,
         B.nodes.insert(B.nodes.begin(), nd);
     }
     nodes.swap(B.nodes);
+    if (bvh_depth(nodes) > (uint32_t)kBvhStack) { // cannot happen with the median tail; kept exact anyway
+        nodes.clear();
+        return false; // the batch walk (exact, no stack bound) traces the meshes
+    }
     leaf_tris.resize(refs_out.size());
     for (size_t k = 0; k < refs_out.size(); ++k) {
         const Prim& p = refs_out[k];
@@ -735,84 +745,20 @@ bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out)
     return true;
 }
 
-// The 48-B form of the quantized nodes (trt_device.h Bvh4CNode).  Checks that every node's
-// inner children are consecutive nodes (collapse_bvh4 numbers them so), then reorders the leaf
-// triangle array node by node — each node's leaf children in slot order, so they are
-// consecutive — and remaps the leaf references of the BVH2 and BVH4 (whose walks read the same
-// array).  Returns false (nothing changed) when a node cannot be expressed: >= 2^20 nodes, a
-// leaf of more than 8 triangles, or non-consecutive inner children.
-bool compress_bvh4(std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4, const std::vector<Bvh4QNode>& q,
-                   std::vector<TriGeo>& leaf_tris, std::vector<Bvh4CNode>& out) {
-    if (b4.empty() || b4.size() != q.size() || b4.size() >= kBvh4cMaxNodes) return false;
-    auto leaf_count = [](uint32_t r) { return ((r >> kBvhCountShift) & 15u) + 1u; };
-    std::vector<TriGeo> tris2;
-    tris2.reserve(leaf_tris.size());
-    std::unordered_map<uint32_t, uint32_t> first_map; // old leaf first -> new first
-    std::vector<Bvh4CNode> c(b4.size());
-    for (size_t n = 0; n < b4.size(); ++n) {
-        const Bvh4Node& nd = b4[n];
-        uint32_t base = 0, k_inner = 0, meta = 0;
-        const uint32_t tri_base = (uint32_t)tris2.size();
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t r = nd.child[i];
-            uint32_t m = 0;
-            if (r == kBvh4None) {
-                m = 0;
-            } else if (!(r & kBvhLeafBit)) {
-                if (k_inner == 0) base = r;
-                if (r != base + k_inner || r >= kBvh4cMaxNodes) return false;
-                ++k_inner;
-                m = 1;
-            } else {
-                const uint32_t cnt = leaf_count(r), first = r & kBvhFirstMask;
-                if (cnt > kBvh4cMaxLeaf || first + cnt > leaf_tris.size()) return false;
-                first_map[first] = (uint32_t)tris2.size();
-                tris2.insert(tris2.end(), leaf_tris.begin() + first, leaf_tris.begin() + first + cnt);
-                m = 2u | ((cnt - 1u) << 2);
-            }
-            meta |= m << (5 * i);
-        }
-        Bvh4CNode& o = c[n];
-        const Bvh4QNode& qq = q[n];
-        for (int a = 0; a < 3; ++a) {
-            o.p[a] = qq.p[a];
-            o.qlo[a] = qq.qlo[a];
-            o.qhi[a] = qq.qhi[a];
-        }
-        o.exps_meta = (qq.exps & 0xFFFFFFu) | ((meta & 0xFFu) << 24);
-        o.base_meta = (base & 0xFFFFFu) | ((meta >> 8) << 20);
-        o.tri_base = tri_base;
+// Levels of the deepest leaf of the BVH2 (root = 1): the BVH2 walk's stack holds at most
+// depth - 1 entries, so build_bvh keeps depth <= kBvhStack.
+uint32_t bvh_depth(const std::vector<BvhNode>& b2) {
+    if (b2.empty()) return 0;
+    uint32_t best = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 1u}};
+    while (!st.empty()) {
+        const auto [n, d] = st.back();
+        st.pop_back();
+        best = std::max(best, d);
+        for (uint32_t c : b2[n].child)
+            if (c != kBvh4None && !(c & kBvhLeafBit)) st.push_back({c, d + 1});
     }
-    if (tris2.size() != leaf_tris.size()) return false; // every triangle sits in exactly one leaf
-    auto remap = [&](uint32_t r) {
-        if (r == kBvh4None || !(r & kBvhLeafBit)) return r;
-        const auto it = first_map.find(r & kBvhFirstMask);
-        return it == first_map.end() ? r : ((r & ~kBvhFirstMask) | it->second);
-    };
-    // self-check: the kernel's decode of every node gives the remapped references slot by slot,
-    // and every leaf holds the same triangles as before
-    for (size_t n = 0; n < b4.size(); ++n) {
-        const uint4 ch = bvh4c_children(c[n].exps_meta, c[n].base_meta, c[n].tri_base);
-        const uint32_t got[4] = {ch.x, ch.y, ch.z, ch.w};
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t old_r = b4[n].child[i], want = remap(old_r);
-            if (got[i] != want) return false;
-            if (want != kBvh4None && (want & kBvhLeafBit)) {
-                const uint32_t cnt = leaf_count(want);
-                for (uint32_t k = 0; k < cnt; ++k)
-                    if (std::memcmp(&tris2[(want & kBvhFirstMask) + k], &leaf_tris[(old_r & kBvhFirstMask) + k],
-                                    sizeof(TriGeo)) != 0)
-                        return false;
-            }
-        }
-    }
-    for (auto& nd : b4)
-        for (auto& r : nd.child) r = remap(r);
-    for (auto& nd : b2)
-        for (auto& r : nd.child) r = remap(r);
-    leaf_tris.swap(tris2);
-    out.swap(c);
-    return true;
+    return best;
 }
 
 } // namespace trt

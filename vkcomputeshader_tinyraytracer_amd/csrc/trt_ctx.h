@@ -33,7 +33,6 @@ struct trt_ctx {
     trt::BvhNode* d_bvh = nullptr;  // per-ray BVH over the triangles (null: batch walk only)
     trt::Bvh4Node* d_bvh4 = nullptr; // the same, 4-wide
     trt::Bvh4QNode* d_bvh4q = nullptr; // the same, 4-wide with quantized child boxes
-    trt::Bvh4CNode* d_bvh4c = nullptr; // the same in 48 B (implicit children)
     trt::TriGeo* d_bvh_tris = nullptr;
     uint32_t node_off[11] = {0};
     uint32_t top = 0;
@@ -55,9 +54,6 @@ struct trt_ctx {
     void* d_rays = nullptr;
     size_t caprays = 0;
     unsigned long long* d_counters = nullptr;
-    // per in-flight slot: per-XCD tile counters of the persistent-grid experiment (TRT_PERSIST
-    // builds, trt_kernel.hip); the last wave of a frame resets them
-    uint32_t* d_persist = nullptr;
     uint32_t num_cus = 256;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> fev; // per-launch event pairs of the last timed trt_render_frames
@@ -73,16 +69,11 @@ struct trt_ctx {
     uint32_t defer_in_flight = 16; // auto frames in flight of deferred-shadow loops (TRT_DEFER_IN_FLIGHT env)
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;
-    // Deferred-frame design (trt_set_defer_design): TRT_DEFER_POOL (rounds 2-4, default),
-    // TRT_DEFER_LEVELS (breadth first, inline shadow rays), TRT_DEFER_LEVELS_B (breadth first,
-    // shadow rays in pass B).  TRT_DEFER_MODE env: "pool" / "levels" / "levels_b".
-    int defer_design = TRT_DEFER_POOL;
-    // pass-A waves per tile of the pool design: 0 = auto (2 when <= 4 frames overlap, else 1),
+    // pass-A waves per tile of a deferred frame: 0 = auto (2 when <= 4 frames overlap, else 1),
     // TRT_DEFER_PPW = 64 / 32 / 16 pixels per wave forces 1 / 2 / 4
     uint32_t defer_sub = 0;
     uint32_t cur_in_flight = 1; // frames in flight of the current render call
     bool spp_lanes = true;      // spp > 1 frames: one lane per sample (TRT_SPP_LANES)
-    bool hot_first = false;     // single-frame plain launches deal last frame's costliest tiles first (TRT_HOT_FIRST)
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.
@@ -102,25 +93,8 @@ struct trt_ctx {
         uint32_t* fb = nullptr;
         trt::DeferCtr* dctr = nullptr;
         size_t ev_chunks = 0, shq_cap = 0, dnpx = 0;
-        // Level-mode deferred scratch (trt_device.h LevCtr): events (20 B each), the two level
-        // queues (32 B per entry), per-pixel fallback flags, the counters.
-        float4* lv_ev = nullptr;
-        uint32_t* lv_evr = nullptr;
-        float4* lv_q[2] = {nullptr, nullptr};
-        uint32_t* lv_qlink[2] = {nullptr, nullptr};
-        trt::LevCtr* lv_ctr = nullptr;
-        uint32_t* lv_flag = nullptr;
-        size_t lv_evcap = 0, lv_qcap = 0, lv_npx = 0;
-        // Hot-first dealing state of single-frame plain launches (KArgs::hot): three lists of
-        // (count, longest wave, hot_max tiles) and three per-tile flag arrays, the tiling they
-        // index, the rotation counter, and the stream that owns them (only frames on that
-        // stream use them: stream order sequences their reads and writes).
-        uint32_t* hot = nullptr;
-        uint8_t* hot_flag = nullptr;
-        uint32_t hot_max = 0, hot_tiles = 0, hot_cap = 0, hot_k = 0;
-        hipStream_t hot_stream = nullptr;
-        bool last_levels = false; // the slot's last deferred frame ran TRT_DEFER_LEVELS
-        size_t last_npx = 0;
+        // per-stripe capacities the slot's last deferred frame ran with (trt_defer_stats)
+        size_t used_ev_cap = 0, used_shq_cap = 0;
         // The stream of the slot's last frame and an event after it: a frame on another
         // stream waits for it before reusing the scratch (trt_render on alternating
         // streams, e.g. dist.PipelinedTiles, must not race on the task queues).
@@ -135,11 +109,9 @@ struct trt_ctx {
     hipEvent_t fork_ev = nullptr;
     uint32_t fev_frames = 0;
     // bytes of each scene binding on the device (trt::kSceneBuf* order), for the broadcast
-    size_t scene_bytes[11] = {0};
+    size_t scene_bytes[10] = {0};
     void* diag = nullptr; // diagnostic builds: ray-dump buffer (trt_diag_set_buffer)
 };
-
-constexpr size_t kPersistWords = 8 * 32; // 8 XCDs x (ticket, done) on their own 128-B lines
 
 namespace trt {
 
@@ -164,7 +136,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
 // The scene bindings of a context in a fixed order (the RCCL scene broadcast walks them).
 enum SceneBuf : int {
     kSceneBatches = 0, kSceneNodes, kSceneBvh, kSceneBvh4, kSceneBvhTris, kSceneGeo, kSceneShade,
-    kSceneMats, kSceneEnv, kSceneBvh4Q, kSceneBvh4C, kSceneBufs
+    kSceneMats, kSceneEnv, kSceneBvh4Q, kSceneBufs
 };
 static_assert(kSceneBufs == sizeof(trt_ctx::scene_bytes) / sizeof(size_t), "one byte count per scene binding");
 void** scene_buf(trt_ctx* c, int k);

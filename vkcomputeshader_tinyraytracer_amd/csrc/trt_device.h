@@ -92,42 +92,6 @@ struct alignas(16) Bvh4QNode {
 };
 static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode is 64 B");
 
-// The quantized node in 48 B (3 x dwordx4 per visit instead of 4): the child references are
-// implicit.  A node's inner children are consecutive nodes from `base` on (collapse_bvh4's BFS
-// numbering), and its leaf children's triangles are consecutive from `tri_base` on (the leaf
-// triangle array is reordered node by node, compress_bvh4).  Per slot i, 5 bits of `meta`
-// (bits 5i .. 5i+4): kind (0 unused, 1 inner, 2 leaf) | (leaf triangles - 1) << 2.  The 20
-// meta bits ride in the spare top byte of the exponent word (bits 0-7) and above a 20-bit
-// `base` (bits 8-19).  Same boxes as Bvh4QNode (bit-identical planes), same node indices.
-constexpr uint32_t kBvh4cMaxNodes = 1u << 20;
-constexpr uint32_t kBvh4cMaxLeaf = 8u;
-struct alignas(16) Bvh4CNode {
-    float p[3];
-    uint32_t exps_meta;  // e_x | e_y << 8 | e_z << 16 | meta[0:8] << 24
-    uint32_t qlo[3];
-    uint32_t qhi[3];
-    uint32_t base_meta;  // first inner child (20 bits) | meta[8:20] << 20
-    uint32_t tri_base;   // first triangle of the leaf children
-};
-static_assert(sizeof(Bvh4CNode) == 48, "Bvh4CNode is 3 x dwordx4");
-
-// Child references of a 48-B node (kBvh4None, an inner node index, or a leaf reference as in
-// BvhNode): inner children consecutive from base, leaf children's triangles consecutive from
-// tri_base, in slot order.  Shared by the kernel's walk and the builder's self-check.
-__host__ __device__ inline uint4 bvh4c_children(uint32_t exps_meta, uint32_t base_meta, uint32_t tri_base) {
-    const uint32_t meta = (exps_meta >> 24) | ((base_meta >> 20) << 8);
-    uint32_t nb = base_meta & 0xFFFFFu, tb = tri_base;
-    uint32_t r[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t m = (meta >> (5 * i)) & 31u;
-        const uint32_t kind = m & 3u, cm1 = m >> 2;
-        r[i] = kind == 1u ? nb : kind == 2u ? (kBvhLeafBit | (cm1 << kBvhCountShift) | tb) : kBvh4None;
-        nb += kind == 1u ? 1u : 0u;
-        tb += kind == 2u ? cm1 + 1u : 0u;
-    }
-    return make_uint4(r[0], r[1], r[2], r[3]);
-}
 
 struct Mat {
     float albedo[4];
@@ -193,23 +157,6 @@ struct DeferCtr {
     uint32_t nq[kDeferStripes * kCtrStride];       // [s * kCtrStride]: queries appended to stripe s
 };
 
-// Deferred frame, LEVEL mode (round 5, trt_kernel.hip level_kernel): the frame's segments are
-// traced breadth first, one launch per tree depth.  Level 0 is the primary rays (one lane per
-// pixel, 8x8 tiles); the children a level makes are appended to the next level's queue, so every
-// launch traces full waves of segments of ONE depth instead of a tile's lanes waiting for its
-// deepest pixel.  Shadow rays are traced inline, so a segment's colour term is final when its
-// event is written: an event is 20 B (term rgb + reflection child slot, and the refraction child
-// slot), where the pool design logged kd, diffuse / specular terms and weights (64 B) plus a 32-B
-// shadow query per light.  Event slots are implicit: level-0 segment of compact pixel o has slot
-// o; level k >= 1 entry i has slot base_k + i, base_1 = npx, base_{k+1} = base_k + n_k, so a
-// parent knows its children's slots when it queues them.  Pass C walks each pixel's tree in the
-// reference's pop order (node, reflection subtree, refraction subtree: shader.comp:530-575).
-// Queue entry: 2 x float4 = (o.xyz, d.x), (d.y, d.z, thr, output pixel).
-struct LevCtr {
-    uint32_t n[(kMaxTreeDepth + 1u) * kCtrStride];    // [k * kCtrStride]: entries appended to level k's queue
-    uint32_t take[(kMaxTreeDepth + 1u) * kCtrStride]; // [k * kCtrStride]: 64-entry chunks taken from it
-};
-
 struct SphereArg {
     float c[3];
     float r;
@@ -260,7 +207,6 @@ struct KArgs {
     const BvhNode* __restrict__ bvh;  // per-lane BVH over triangles, or null (batch walk)
     const Bvh4Node* __restrict__ bvh4; // the same BVH collapsed to 4-wide nodes
     const Bvh4QNode* __restrict__ bvh4q; // ... with quantized child boxes (same node indices)
-    const Bvh4CNode* __restrict__ bvh4c; // ... quantized, implicit children, 48 B (used when set)
     const TriGeo* __restrict__ bvh_tris; // BVH-ordered geometry; pad = (triangle, batch, ni)
     const float4* __restrict__ nodes; // batch hierarchy: per node (lo.xyz, -), (hi.xyz, -)
     uint32_t node_off[11];            // first node of level L (L = 1..top) in `nodes`
@@ -268,7 +214,6 @@ struct KArgs {
     uint32_t ntx;                     // 8x8 tiles per output row
     uint32_t ntiles;              // 8x8 tiles in the launch
     uint32_t bvh_waves4;          // BVH walk: the 4-waves-per-SIMD build (GEOM 3)
-    uint32_t bvh4q_n;             // nodes of bvh4q (the walk's LDS copy of the top nodes)
     uint32_t xcd_rot, xcd_skew;   // multi-frame tile dealing (xcd_tile): rotation period, row skew
     uint32_t xcd_inter;           // ... frames interleaved per chunk group (inter_tile); 2: no rotation, permuted classes
     uint32_t xcd_mult;            // ... xcd_inter 2: chunk permutation multiplier (coprime to the dealt chunks)
@@ -291,15 +236,6 @@ struct KArgs {
     unsigned long long* __restrict__ acc; // per output pixel: fixed-point colour (r, g, b, -)
     uint32_t* __restrict__ spilled;   // output pixels finished by finalize_spilled
     float4* __restrict__ diag;        // diagnostic builds only (TRT_DIAG_DUMP_SHADOW): ray dump
-    uint32_t* __restrict__ persist;   // TRT_PERSIST builds: per-XCD tile tickets of this slot
-    // Hot-first dealing of single-frame plain launches (trace_hot): blocks [0, hot_max) trace
-    // the tiles the slot's previous frame found costliest, the others the remaining tiles in
-    // xcd_tile order.  hot: three lists of (count, longest wave duration, hot_max tiles), used
-    // in rotation (read hot_k % 3, write (hot_k + 1) % 3, clear (hot_k + 2) % 3); hot_flag: three
-    // per-tile flag arrays of hot_fstride bytes (1 = in that list).  hot_max = 0: off.
-    uint32_t* __restrict__ hot;
-    uint8_t* __restrict__ hot_flag;
-    uint32_t hot_max, hot_k, hot_fstride;
     // deferred shadows (defer != 0): event log, shadow query queue, per-pixel log heads
     uint32_t defer;
     uint32_t ev_cap;                  // event chunks per stripe (stripe s: chunks [s * ev_cap, ...))
@@ -311,17 +247,6 @@ struct KArgs {
     DeferCtr* __restrict__ dctr;
     uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4: trace_tile)
     uint32_t spp_lanes;               // spp > 1: one lane per sample (trace_samples), spp waves per tile
-    // deferred frames, level mode (lv != 0): see LevCtr
-    uint32_t lv;                      // level mode: 1 = shadow rays inline, 2 = shadows in pass B
-    uint32_t lv_level;                // the depth this launch traces (level_kernel)
-    uint32_t lv_qcap;                 // entries per level queue
-    uint32_t lv_evcap;                // event slots
-    float4* __restrict__ lv_ev;       // per event slot: term rgb, reflection child slot (kEvNone: none)
-    uint32_t* __restrict__ lv_evr;    // per event slot: refraction child slot
-    float4* __restrict__ lv_q[2];     // level k's queue: lv_q[k & 1], 2 float4 per entry
-    uint32_t* __restrict__ lv_qlink[2]; // lv == 2: per entry, its parent link (slot << 1 | refraction)
-    LevCtr* __restrict__ lv_ctr;
-    uint32_t* __restrict__ lv_flag;   // per compact pixel: 1 = handed to defer_fallback
     FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch
 };
 static_assert(sizeof(KArgs) <= 4096, "KArgs fits the 4 KB kernel-argument limit");

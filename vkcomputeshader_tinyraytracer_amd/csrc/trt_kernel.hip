@@ -32,21 +32,9 @@
 
 namespace trt {
 
-// Waves per workgroup of the tile kernel (each wave traces its own 8x8 tile; no barriers).
-#ifndef TRT_WPB
-#define TRT_WPB 1
-#endif
-// Orders one wave's LDS accesses (the slab is private to the wave).
-__device__ __forceinline__ void wave_lds_sync() {
-    if (TRT_WPB == 1) {
-        __syncthreads(); // one wave per workgroup
-    } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-__device__ __forceinline__ uint32_t lane_id() { return TRT_WPB == 1 ? threadIdx.x : (threadIdx.x & 63u); }
+// Orders one wave's LDS accesses (one wave per workgroup: the slab is private to the wave).
+__device__ __forceinline__ void wave_lds_sync() { __syncthreads(); }
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
 // Rank of this lane among the set bits of `mask` below it.
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -141,36 +129,6 @@ __device__ __forceinline__ bool sphere_hit(f3 o, f3 d, const SphereArg& s, float
     f3 L = sub(mk(s.c[0], s.c[1], s.c[2]), o);
     float tca = dot3(L, d);
     float d2 = dot3(L, L) - tca * tca;
-    float r2 = s.r * s.r;
-    if (d2 > r2) return false;
-    float thc = sqrt_rn(r2 - d2);
-    float t0 = tca - thc, t1 = tca + thc;
-    if (t0 > TRT_EPS) t = t0;
-    else if (t1 > TRT_EPS) t = t1;
-    else return false;
-    return true;
-}
-
-// Two spheres' ray_sphere_intersect prologue in packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two
-// IEEE operations per instruction, each rounded as its scalar form, no contraction): L = c - o,
-// tca = dot(L, d), d2 = dot(L, L) - tca * tca in sphere_hit's operand order, so every element is
-// sphere_hit's value bit for bit.
-// Measured and rejected (round 5): in scene_intersect alone C2 +5 % (12.8 vs 12.2 us per frame at
-// 20-frame launches, profiles/r05i_ab_sphere_pk.jsonl: the packed operands cost register moves
-// and pairs at the 96-VGPR cap); in shadow_intersect it spills the C2 kernel (60 B).
-#ifndef TRT_SPHERE_PK
-#define TRT_SPHERE_PK 0 /* bit 0: scene_intersect, bit 1: shadow_intersect */
-#endif
-typedef float pk2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void sphere_pair_pre(f3 o, f3 d, const SphereArg& s0, const SphereArg& s1, pk2& tca, pk2& d2) {
-    const pk2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const pk2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
-    const pk2 Lx = pk2{s0.c[0], s1.c[0]} - ox, Ly = pk2{s0.c[1], s1.c[1]} - oy, Lz = pk2{s0.c[2], s1.c[2]} - oz;
-    tca = (Lx * dx + Ly * dy) + Lz * dz;
-    d2 = ((Lx * Lx + Ly * Ly) + Lz * Lz) - tca * tca;
-}
-// sphere_hit's remainder from its prologue's tca and d2
-__device__ __forceinline__ bool sphere_hit_post(const SphereArg& s, float tca, float d2, float& t) {
     float r2 = s.r * s.r;
     if (d2 > r2) return false;
     float thc = sqrt_rn(r2 - d2);
@@ -418,32 +376,6 @@ constexpr int bvh_lds_entries() { return GEOM == 3 ? (TRT_BVH_LDS ? TRT_G3_LDS :
 // 32-bit words of a wave's BVH-stack LDS (slab_float4s below holds them)
 template <int GEOM>
 constexpr int slab_words() { return bvh_lds_entries<GEOM>() * 64; }
-// TRT_TOP_LDS: the wave keeps the first K nodes of the quantized BVH4 in its LDS (the nodes are
-// numbered breadth first: the root, its children, their children: K = 21 is the top three
-// levels of a full tree), copied once when the wave starts; a lane whose walk stands on one of
-// them reads it with ds_read_b128 instead of four per-lane global loads through TA / TD (the
-// walk is bound by the vector-memory pipe).  Wave-uniform visits keep their scalar fetch.
-// The slab holds, after the traversal stack, one header float4 (x = the nodes copied) and the
-// nodes; every kernel with a GEOM 3 slab fills it (top_fill) before its first walk.
-// Measured and rejected (round 5, profiles/r05r_ab_top_lds.jsonl, same box, two rounds): K = 21
-// C4 +0.6 %, C3 +2 %, C5 +0.6 %, the shipped frame +3 %, the README scene +7 %; K = 5 within
-// +-1.5 % of none.  The top levels' visits are mostly wave-uniform (one scalar fetch already),
-// and the extra LDS and the per-lane LDS / global select cost more than the TA / TD cycles the
-// divergent top visits save.  Off (0 compiles it out).
-#ifndef TRT_TOP_LDS
-#define TRT_TOP_LDS 0
-#endif
-// pass A of deferred frames (4 waves per SIMD with the 5-KB segment pool): the top two levels
-// only; split launches (LDS segment stacks) keep none
-#ifndef TRT_TOP_LDS_DEFER
-#define TRT_TOP_LDS_DEFER 5
-#endif
-template <int GEOM, bool DEFER = false>
-constexpr int top_nodes() { return GEOM == 3 ? (DEFER ? TRT_TOP_LDS_DEFER : TRT_TOP_LDS) : 0; }
-// float4 offset of the header in a GEOM 3 slab
-template <int GEOM>
-constexpr int top_off() { return bvh_lds_entries<GEOM>() * 16; }
-
 // PUSH3: the branch-free push of up to three children (push_sorted) — used by the 3-wave
 // build: C3 -4 %, shipped frame -6 %; the 4-wave build (128-VGPR cap) is 3 % slower with it
 // (profiles/r01_ab_push3.log).
@@ -813,23 +745,6 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 #ifndef TRT_UNIFORM_NODE
 #define TRT_UNIFORM_NODE 1
 #endif
-// 48-B nodes with implicit children (trt_device.h Bvh4CNode): measured slower than the 64-B
-// quantized nodes on C4 (+5 %) and neutral elsewhere (profiles/r03_ab_c4_walk.log), so the walk
-// is compiled only on request (-DTRT_BVH_COMPRESS=1, with TRT_BVH_COMPRESS=1 at upload).
-#ifndef TRT_BVH_COMPRESS
-#define TRT_BVH_COMPRESS 0
-#endif
-// Loop shape of the quantized walk: 0 = one node or one leaf per iteration (if-if),
-// 1 = while-while, 2 = speculative while-while (leaves parked until the wave has one each).
-#ifndef TRT_WHILE_WHILE
-#define TRT_WHILE_WHILE 0
-#endif
-// Shadow walks share found occluders across the wave (trace_bvh4's quantized walk, below).
-// Measured: C4 +0.7 %, C3 / shipped / README within noise (profiles/r03_ab_shadow_share.log;
-// the C4 shadow walks are long where they find nothing, not where they find late), so off.
-#ifndef TRT_SHADOW_SHARE
-#define TRT_SHADOW_SHARE 0
-#endif
 // GEOM 3 kernels walk the quantized nodes only (the host picks GEOM 3 only when they exist):
 // the 64-B-node and binary walks are not compiled into them, so the register allocation of
 // the 96-VGPR (5-wave) build sees one walk per call site.
@@ -837,7 +752,7 @@ __device__ __forceinline__ bool visit4q(f3 o, f3 inv, float best, const float4& 
 #define TRT_G3_QONLY 1
 #endif
 template <int GEOM>
-constexpr bool g3_quant_only() { return GEOM == 3 && TRT_G3_QONLY && TRT_BVH_QUANT && !TRT_BVH_COMPRESS; }
+constexpr bool g3_quant_only() { return GEOM == 3 && TRT_G3_QONLY && TRT_BVH_QUANT; }
 template <bool COUNT, bool SHADOW, int GEOM>
 __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, Hit& h, bool& occluded,
                                            float max_dist, Cnt& c, float4* slab) {
@@ -846,61 +761,6 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
     Stack stack(slab, stack_mem);
     uint32_t node = 0;
     float best = SHADOW ? max_dist : h.t;
-#if TRT_BVH_COMPRESS
-    // 48-B quantized nodes (3 x dwordx4 per visit): the walk of the quantized nodes below with
-    // the child references rebuilt from the node's implicit layout (the host sets bvh4c only for
-    // the builds it measured faster with them)
-    if (A.bvh4c) {
-        {
-            typedef __attribute__((address_space(4))) const float cfloat;
-            typedef __attribute__((address_space(4))) const uint32_t cuint;
-            const cfloat* R = (const cfloat*)(A.bvh4c);
-            const cuint* RC = (const cuint*)(A.bvh4c);
-            const float4 pe = make_float4(R[0], R[1], R[2], R[3]);
-            const uint4 qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
-            const uint4 qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
-#ifdef TRT_DIAG_PIXEL_WORK
-            ++c.wn;
-#endif
-            if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, bvh4c_children(RC[3], RC[10], RC[11]), stack, node, c))
-                return;
-        }
-        for (;;) {
-            if (!(node & kBvhLeafBit)) {
-                float4 pe;
-                uint4 qa, qb;
-#if TRT_UNIFORM_NODE
-                const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
-                if (__ballot(node != n0) == 0ull) {
-                    typedef __attribute__((address_space(4))) const float cfloat;
-                    typedef __attribute__((address_space(4))) const uint32_t cuint;
-                    const cfloat* R = (const cfloat*)(A.bvh4c + n0);
-                    const cuint* RC = (const cuint*)(A.bvh4c + n0);
-                    pe = make_float4(R[0], R[1], R[2], R[3]);
-                    qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
-                    qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
-                } else
-#endif
-                {
-                    const float4* p = reinterpret_cast<const float4*>(A.bvh4c + node);
-                    pe = p[0];
-                    qa = reinterpret_cast<const uint4*>(p)[1];
-                    qb = reinterpret_cast<const uint4*>(p)[2];
-                }
-#ifdef TRT_DIAG_PIXEL_WORK
-                ++c.wn;
-#endif
-                const uint4 ch = bvh4c_children(__float_as_uint(pe.w), qb.z, qb.w);
-                if (visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) continue;
-            } else if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
-                occluded = true;
-                return;
-            }
-            if (stack.sp == 0) return;
-            node = stack.pop();
-        }
-    }
-#endif
 #if TRT_BVH_QUANT
     // measured: -3 % on C4 (1,600 batches, 4-wave build), +2..3 % on C3 / the shipped frame
     // (profiles/r02_ab_quant.log), so the quantized nodes serve the 4-wave build only
@@ -919,29 +779,8 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
 #endif
             if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) return;
         }
-        // nodes below ntop are in the wave's LDS (top_fill; 0 when the kernel keeps none)
-        uint32_t ntop = 0u;
-        if constexpr (GEOM == 3 && TRT_TOP_LDS > 0)
-            ntop = __builtin_amdgcn_readfirstlane(((const lds_u32*)reinterpret_cast<uint32_t*>(slab + top_off<GEOM>()))[0]);
         auto fetch = [&](uint32_t nd, float4& pe, uint4& qa, uint4& qb, uint4& ch) {
-#if TRT_UNIFORM_NODE == 2
-            // the first lane's node through scalar loads for every lane standing on it, the
-            // other lanes' nodes through per-lane loads (fewer lanes in the vector-memory pipe)
-            {
-                const uint32_t n0 = __builtin_amdgcn_readfirstlane(nd);
-                typedef __attribute__((address_space(4))) const float cfloat;
-                typedef __attribute__((address_space(4))) const uint32_t cuint;
-                const cfloat* R = (const cfloat*)(A.bvh4q + n0);
-                const cuint* RC = (const cuint*)(A.bvh4q + n0);
-                if (nd == n0) {
-                    pe = make_float4(R[0], R[1], R[2], R[3]);
-                    qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
-                    qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
-                    ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
-                    return;
-                }
-            }
-#elif TRT_UNIFORM_NODE
+#if TRT_UNIFORM_NODE
             // every lane at an internal node visits the same node (coherent rays, top levels):
             // one scalar fetch for the wave instead of 4 per-lane dwordx4 loads through TA/TD
             const uint32_t n0 = __builtin_amdgcn_readfirstlane(nd);
@@ -957,109 +796,12 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
                 return;
             }
 #endif
-            if (GEOM == 3 && TRT_TOP_LDS > 0 && nd < ntop) {
-                const lds_u32* t = (const lds_u32*)reinterpret_cast<uint32_t*>(slab + top_off<GEOM>() + 1u + nd * 4u);
-                pe = make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]), __uint_as_float(t[3]));
-                qa = make_uint4(t[4], t[5], t[6], t[7]);
-                qb = make_uint4(t[8], t[9], t[10], t[11]);
-                ch = make_uint4(t[12], t[13], t[14], t[15]);
-                return;
-            }
             const float4* p = reinterpret_cast<const float4*>(A.bvh4q + nd);
             pe = p[0];
             qa = reinterpret_cast<const uint4*>(p)[1];
             qb = reinterpret_cast<const uint4*>(p)[2];
             ch = reinterpret_cast<const uint4*>(p)[3];
         };
-#if TRT_WHILE_WHILE == 1
-        // while-while: the wave descends inner nodes until every lane stands on a leaf (or has
-        // finished), then tests the leaves together
-        for (;;) {
-            while (!(node & kBvhLeafBit)) {
-                float4 pe;
-                uint4 qa, qb, ch;
-                fetch(node, pe, qa, qb, ch);
-#ifdef TRT_DIAG_PIXEL_WORK
-                ++c.wn;
-#endif
-                if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c)) {
-                    if (stack.sp == 0) return;
-                    node = stack.pop();
-                }
-            }
-            if (bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c)) {
-                occluded = true;
-                return;
-            }
-            if (stack.sp == 0) return;
-            node = stack.pop();
-        }
-#elif TRT_WHILE_WHILE == 2
-        // speculative while-while: a lane that reaches a leaf parks it and keeps descending
-        // until every lane still walking has parked one (or reaches a second leaf), then the
-        // parked leaves are tested together
-        for (;;) {
-            uint32_t parked = kBvh4None;
-            for (;;) {
-                if (node == kBvh4None) break;
-                if (node & kBvhLeafBit) {
-                    if (parked != kBvh4None) break;
-                    parked = node;
-                    node = stack.sp ? stack.pop() : kBvh4None;
-                } else {
-                    float4 pe;
-                    uint4 qa, qb, ch;
-                    fetch(node, pe, qa, qb, ch);
-#ifdef TRT_DIAG_PIXEL_WORK
-                    ++c.wn;
-#endif
-                    if (!visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c))
-                        node = stack.sp ? stack.pop() : kBvh4None;
-                }
-                const bool searching = parked == kBvh4None;
-                if (__ballot(searching) == 0ull) break;
-            }
-            if (parked != kBvh4None && bvh_leaf<COUNT, SHADOW>(A, parked, o, d, inv, h, max_dist, best, c)) {
-                occluded = true;
-                return;
-            }
-            if (node == kBvh4None) return;
-        }
-#else
-#if TRT_SHADOW_SHARE
-        if constexpr (SHADOW && !COUNT) {
-            // Shared occluders: when lanes find an occluder in a step, every lane still walking
-            // tests the first one's triangle (scalar loads, no vector-memory instruction) and
-            // leaves if it is occluded by it too.  Neighbouring shading points asking about the
-            // same light are mostly shadowed by the same triangle, so one lane's find ends most
-            // of the wave's walks.  Any hit answers a shadow query (order-free) and the shared
-            // test is the leaf test itself, so the answer is the per-lane walk's.
-            for (;;) {
-                bool hit = false, more = false;
-                if (!(node & kBvhLeafBit)) {
-                    float4 pe;
-                    uint4 qa, qb, ch;
-                    fetch(node, pe, qa, qb, ch);
-                    more = visit4q<COUNT>(o, inv, best, pe, qa, qb, ch, stack, node, c);
-                } else {
-                    hit = bvh_leaf<COUNT, SHADOW>(A, node, o, d, inv, h, max_dist, best, c);
-                }
-                const uint64_t m = __ballot(hit);
-                if (m != 0ull) {
-                    const uint32_t k = __builtin_amdgcn_readlane((uint32_t)h.idx, (int)__builtin_ctzll(m));
-                    if (!hit) hit = shadow_tri_s(A, k, o, d, max_dist);
-                    if (hit) {
-                        occluded = true;
-                        return;
-                    }
-                }
-                if (!more) {
-                    if (stack.sp == 0) return;
-                    node = stack.pop();
-                }
-            }
-        }
-#endif
         for (;;) {
             if (!(node & kBvhLeafBit)) {
                 float4 pe;
@@ -1076,7 +818,6 @@ __device__ __forceinline__ void trace_bvh4(const KArgs& A, f3 o, f3 d, f3 inv, H
             if (stack.sp == 0) return;
             node = stack.pop();
         }
-#endif
     }
 #endif
     if constexpr (g3_quant_only<GEOM>()) return;
@@ -1172,14 +913,6 @@ __device__ __forceinline__ bool ray_misses_all_batches(f3 o, f3 d) {
 #endif
 #ifndef TRT_SHADOW_WAVE_EXT
 #define TRT_SHADOW_WAVE_EXT 0.1
-#endif
-// TRT_SHADOW_SUBSET (min lanes, 0 = off): a wave whose shadow origins are not all near its first
-// lane's lets the near ones walk together (shadow_wave_q) and the rest alone.  Measured and
-// rejected (round 5, profiles/r05ac_ab_shadow_subset.jsonl): 8 / 16 / 32 lanes: C4 +12 / +10 /
-// +7 %, the shipped frame +16 / +11 / +5 % at 16 in flight — the two phases run one after the
-// other, and the lone walks are hardly shorter for having fewer lanes.
-#ifndef TRT_SHADOW_SUBSET
-#define TRT_SHADOW_SUBSET 0
 #endif
 constexpr int kShadowWaveStack = 128; // >= kBvhStack
 __device__ __forceinline__ bool shadow_wave_q(const KArgs& A, f3 o, f3 d, f3 inv, float max_dist, float4* slab) {
@@ -1286,19 +1019,11 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
         }
     }
     if (A.flags & TRT_FLAG_SPHERES) { // shader.comp:322-335
-#if TRT_SPHERE_PK & 1
-        pk2 tca, d2;
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = 1e10f;
             if (COUNT) ++c.sph;
-#if TRT_SPHERE_PK & 1
-            if ((i & 1) == 0) sphere_pair_pre(o, d, A.sph[i], A.sph[i + 1], tca, d2);
-            const bool hit = sphere_hit_post(A.sph[i], tca[i & 1], d2[i & 1], t);
-#else
             const bool hit = sphere_hit(o, d, A.sph[i], t);
-#endif
             if (hit && t < h.t) {
                 h.t = t;
                 h.kind = HIT_SPHERE;
@@ -1338,19 +1063,11 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
     }
 #endif
     if (A.flags & TRT_FLAG_SPHERES) {
-#if TRT_SPHERE_PK & 2
-        pk2 tca, d2;
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = 1e10f;
             if (COUNT) ++c.sph;
-#if TRT_SPHERE_PK & 2
-            if ((i & 1) == 0) sphere_pair_pre(o, d, A.sph[i], A.sph[i + 1], tca, d2);
-            if (sphere_hit_post(A.sph[i], tca[i & 1], d2[i & 1], t) && t < max_dist) return true;
-#else
             if (sphere_hit(o, d, A.sph[i], t) && t < max_dist) return true;
-#endif
         }
     }
     if (GEOM == 0 || A.nbatch == 0) return false;
@@ -1372,10 +1089,6 @@ __device__ __forceinline__ bool shadow_intersect(const KArgs& A, f3 o, f3 d, flo
                 const bool near = e <= (float)TRT_SHADOW_WAVE_EXT;
                 const uint64_t nm = __ballot(near);
                 if (nm == __ballot(true)) return shadow_wave_q(A, o, d, inv, max_dist, slab);
-                // TRT_SHADOW_SUBSET: when at least that many lanes lie near the first one, those
-                // lanes walk together and only the others walk alone
-                if (TRT_SHADOW_SUBSET > 0 && __popcll(nm) >= (uint32_t)TRT_SHADOW_SUBSET && near)
-                    return shadow_wave_q(A, o, d, inv, max_dist, slab);
             }
 #endif
         if (g3_quant_only<GEOM>() || (TRT_BVH_WIDTH == 4 && A.bvh4)) trace_bvh4<COUNT, true, GEOM>(A, o, d, inv, unused, occluded, max_dist, c, slab);
@@ -1534,26 +1247,8 @@ template <int CAP, int GEOM = 0, bool HYB = false>
 constexpr bool seg_lds() { return CAP >= 1 && CAP <= LDS_STACK_MAX && (HYB || !(GEOM == 3 && TRT_G3_SEG_PRIV)); }
 template <int CAP, int GEOM = 0, bool HYB = false>
 constexpr int lds_stack_floats_() { return seg_lds<CAP, GEOM, HYB>() ? CAP * 8 * 64 : 1; }
-// TRT_G3_PARK: with the deferred children out of LDS, the GEOM 3 per-pixel loop parks the
-// shading state its shadow walks do not use (colour, throughput, depth, the child weights and
-// index of refraction, the ray direction, kd, the exponent, the diffuse weight: 16 floats per
-// lane, 4 KB per wave) in LDS around the walks, instead of the register allocator spilling it to
-// scratch (the 96-VGPR 5-wave build).  Measured: the static spill reloads fall (232 -> 164) but
-// C4 +6.4 %, C3 +6.3 %, the README scene +3.6 % (profiles/r04s_ab_g3_park_rejected.jsonl: the
-// compiler-level fences and LDS round trips cost more than the scratch they replace), so off.
-#ifndef TRT_G3_PARK
-#define TRT_G3_PARK 0
-#endif
-constexpr int kParkFields = 16;
-template <int GEOM, bool HYB>
-constexpr bool park_state() { return GEOM == 3 && TRT_G3_PARK && TRT_G3_SEG_PRIV && !HYB; }
 template <int CAP, int GEOM = 0, bool HYB = false>
-constexpr int lds_stack_floats() {
-    return park_state<GEOM, HYB>() ? kParkFields * 64 : lds_stack_floats_<CAP, GEOM, HYB>();
-}
-// A compiler-only memory barrier: parked values are read back from LDS, not forwarded from the
-// registers that stored them (which would keep them live across the walks).
-__device__ __forceinline__ void park_fence() { asm volatile("" ::: "memory"); }
+constexpr int lds_stack_floats() { return lds_stack_floats_<CAP, GEOM, HYB>(); }
 
 template <int CAP, bool LDS = (CAP <= LDS_STACK_MAX)>
 struct DeferStack;
@@ -1892,29 +1587,14 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
 #ifdef TRT_DIAG_PIXEL_WORK
         ++cnt.wseg;
 #endif
-#ifdef TRT_PRIO
-        if (cur.depth > 0) __builtin_amdgcn_s_setprio(TRT_PRIO);
-#endif
         Hit h;
         scene_intersect<COUNT, GEOM>(A, cur.o, cur.d, h, cnt, slab);
         bool have_next = false;
         Seg next;
-#ifdef TRT_BG_EARLY
-        // Miss lanes issue their envmap gather before the hit lanes' shading and consume it
-        // after: the texel latency hides under the shading the wave executes meanwhile.  Each
-        // lane adds exactly one contribution per segment, so the sum order is unchanged.
-        const bool env_miss = h.kind == HIT_NONE && (A.flags & TRT_FLAG_ENVMAP);
-        EnvFetch ef;
-        if (env_miss) ef = env_fetch(A, cur.d);
-#endif
         if (h.kind == HIT_NONE) {
             if (COUNT) ++cnt.miss;
-#ifdef TRT_BG_EARLY
-            if (!env_miss) color = add(color, muls(mk(0.2f, 0.7f, 0.8f), cur.thr));
-#else
             f3 bg = background(A, cur.d);
             color = add(color, muls(bg, cur.thr));
-#endif
         } else {
             // Resolve the closest hit: point, normal, material (shader.comp:302-360).
             f3 p = add(cur.o, muls(cur.d, h.t));
@@ -1964,7 +1644,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             // Phong with three shadow rays, shader.comp:483-507.
             f3 v = neg(cur.d);
             f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
-            constexpr bool LATE = GEOM >= 2 && TRT_LATE_MAT && !HYB && !park_state<GEOM, HYB>();
+            constexpr bool LATE = GEOM >= 2 && TRT_LATE_MAT && !HYB;
             if constexpr (LATE) {
                 // Phase 1: the three lights' terms (light_term's arithmetic), before any walk.
                 float dif[3], spc[3];
@@ -2026,30 +1706,8 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 for (int k = 0; k < 4; ++k) alb[k] = mv.alb[k];
                 ior = mv.ior;
             }
-            // PARK (GEOM 3): what the light loop does not need during its shadow walks waits in
-            // this lane's LDS column (park_state) and is read back after each walk / the loop.
-            constexpr bool PARK = park_state<GEOM, HYB>();
-            lds_f32* const P = (lds_f32*)(lds + lane_id());
             if constexpr (!LATE) {
             f3 kdv = mk(kd[0], kd[1], kd[2]);
-            if constexpr (PARK) {
-                const float f[kParkFields] = {color.x, color.y, color.z, cur.thr, __int_as_float(cur.depth), alb[2],
-                                              alb[3], ior, cur.d.x, cur.d.y, cur.d.z, kd[0], kd[1], kd[2], sexp, alb[0]};
-#pragma unroll
-                for (int k = 0; k < kParkFields; ++k) P[k * 64] = f[k];
-            }
-            auto park_v = [&]() -> f3 {
-                if constexpr (PARK) return neg(mk(P[8 * 64], P[9 * 64], P[10 * 64]));
-                else return v;
-            };
-            auto park_kd = [&]() -> f3 {
-                if constexpr (PARK) return mk(P[11 * 64], P[12 * 64], P[13 * 64]);
-                else return kdv;
-            };
-            auto park_f = [&](int k, float x) -> float {
-                if constexpr (PARK) return P[k * 64];
-                else return x;
-            };
             // Mesh kernels (GEOM >= 2) keep the light loop rolled: unrolled, each of the three
             // lights inlines its own copy of the shadow walks (the wave-coherent one and the
             // per-lane BVH walk), which multiplied the kernel's code past the instruction cache
@@ -2060,8 +1718,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             constexpr int kLightUnroll = GEOM >= 2 && !TRT_LIGHT_UNROLL ? 1 : 3;
 #pragma unroll kLightUnroll
             for (int i = 0; i < 3; ++i) {
-                if constexpr (PARK) park_fence();
-                const float sexp_i = park_f(14, sexp), alb0_i = park_f(15, alb[0]);
                 f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
                 float dist;
                 f3 ld = normalize_len3(sub(L, p), dist);
@@ -2073,9 +1729,9 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 if (!TRT_SPEC_SKIP || alb[1] != 0.0f) {
                     const f3 rdir = reflect3(neg(ld), n);
 #ifdef TRT_DIAG_NO_POW
-                    spec = 1.0f * fmaxf(0.0f, dot3(rdir, park_v())) * sexp_i; // diagnostic: prices powf
+                    spec = 1.0f * fmaxf(0.0f, dot3(rdir, v)) * sexp; // diagnostic: prices powf
 #else
-                    spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, park_v())), sexp_i);
+                    spec = 1.0f * pow_pos(fmaxf(0.0f, dot3(rdir, v)), sexp);
 #endif
                 }
                 // A light whose diffuse term and specular term both vanish from the colour (a
@@ -2085,13 +1741,12 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 // reference's behaviour (traces it and adds the terms when lit: its counters and
                 // image are the reference's, and tests/test_gpu_parity.py checks that its image
                 // equals the frame's bit for bit) and reports the skipped queries and their work.
-                const bool matters = TRT_SKIP_DARK == 0 || (alb0_i != 0.0f && diff != 0.0f) ||
+                const bool matters = TRT_SKIP_DARK == 0 || (alb[0] != 0.0f && diff != 0.0f) ||
                                      (alb[1] != 0.0f && spec != 0.0f);
                 if (COUNT) ++cnt.sh;
                 if (!COUNT && !matters) continue;
                 const Cnt before = cnt;
                 const bool occl = shadow_intersect<COUNT, GEOM>(A, so, ld, dist, cnt, slab);
-                if constexpr (PARK) park_fence();
                 if (COUNT && !matters) {
                     ++cnt.sk;
                     cnt.ssph += cnt.sph - before.sph;
@@ -2102,22 +1757,10 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                     cnt.stv += cnt.tv - before.tv;
                 }
                 if (occl) continue;
-                const f3 kd_i = park_kd();
-                diffuse = add(diffuse, muls(kd_i, diff));
-                specular = add(specular, muls(kd_i, spec));
+                diffuse = add(diffuse, muls(kdv, diff));
+                specular = add(specular, muls(kdv, spec));
             }
             } // !LATE
-            if constexpr (PARK) {
-                park_fence();
-                color = mk(P[0], P[64], P[128]);
-                cur.thr = P[3 * 64];
-                cur.depth = __float_as_int(P[4 * 64]);
-                alb[2] = P[5 * 64];
-                alb[3] = P[6 * 64];
-                ior = P[7 * 64];
-                cur.d = mk(P[8 * 64], P[9 * 64], P[10 * 64]);
-                alb[0] = P[15 * 64];
-            }
             color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
             // Children (shader.comp:509-575).  Children that the reference would push and
             // then drop unseen at the depth / throughput test (shader.comp:449) are not made.
@@ -2164,9 +1807,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 have_next = true;
             }
         }
-#ifdef TRT_BG_EARLY
-        if (env_miss) color = add(color, muls(env_blend(ef), cur.thr));
-#endif
         if (have_next) {
             cur = next;
         } else if (stk.n > 0) {
@@ -2328,7 +1968,7 @@ __device__ __forceinline__ void defer_shade(const KArgs& A, EvLog& L, uint32_t s
     }
 }
 
-// The wave's pending-segment pool (defer_walk / defer_walk_q): a lane without work takes its
+// The wave's pending-segment pool (defer_walk): a lane without work takes its
 // private overflow first, then the pool's top entries (wave-aggregated, one per idle lane by
 // rank); `want` lanes get work.  pool_n is wave-uniform.
 __device__ __forceinline__ void pool_refill(const lds_f32* P, uint32_t& pool_n, PSeg* priv, int& pn, bool want,
@@ -2402,145 +2042,6 @@ __device__ __forceinline__ void defer_walk(const KArgs& A, float* lds, float4* s
             defer_shade<SPLIT>(A, L, slot, h, cur, link, pix, have, other, have_other);
         }
         pool_offer(P, pool_n, priv, pn, have_other, other);
-    }
-}
-
-// Pass A with the quantized BVH4 walk turned inside out (GEOM 3): the wave advances every
-// traversing lane by ONE node visit or leaf test per step, and a lane whose walk has ended
-// waits until fewer than TRT_REFILL_T lanes still walk; then the finished lanes are shaded
-// together (their events, queries and children) and refilled with new segments (their
-// reflection child, their private overflow, the wave's pool), so a wave no longer runs each
-// step as long as its longest walk (Aila & Laine's dynamic ray fetch).  The walk is
-// trace_bvh4's, visit for visit: the same closest hit.
-// Measured and rejected (round 4, profiles/r04d_ab_deep.jsonl): the shipped frame 442 -> 576 us
-// per frame at 8 in flight (+30 %; thresholds 16 / 48: +24 % / +36 %), pass A 20.8 -> 17.7 lanes
-// active with 32 % more VALU and 50 % more vector-memory instructions per wave (the walk's
-// per-step bookkeeping, and the wave-uniform node fetch rarely fires once lanes are out of
-// step).  Kept as an opt-in experiment.
-#ifndef TRT_DEFER_REFILL
-#define TRT_DEFER_REFILL 0
-#endif
-#ifndef TRT_REFILL_T
-#define TRT_REFILL_T 32
-#endif
-template <int GEOM>
-constexpr bool defer_refill() {
-    return GEOM == 3 && TRT_DEFER_REFILL && !TRT_BVH_COMPRESS && TRT_BVH_QUANT && TRT_BVH_WIDTH == 4;
-}
-__device__ __forceinline__ bool defer_use_q(const KArgs& A) { return A.bvh4 && A.bvh4q && A.nbatch != 0; }
-template <bool SPLIT>
-__device__ __forceinline__ void defer_walk_q(const KArgs& A, float* lds, float4* slab, EvLog& L, bool have, Seg cur,
-                                             uint32_t link, uint32_t pix) {
-    lds_f32* P = (lds_f32*)lds;
-    Cnt cnt;
-    PSeg priv[kMaxTreeDepth];
-    int pn = 0;
-    uint32_t pool_n = 0; // wave-uniform
-    using Stack = BvhStack<bvh_lds_entries<3>(), false>;
-    typename Stack::Mem stack_mem;
-    Stack stack(slab, stack_mem);
-    enum : int { IDLE = 0, START = 1, TRAV = 2, DONE = 3 };
-    int ph = have ? START : IDLE;
-    Hit h;
-    h.kind = HIT_NONE;
-    f3 inv = mk(0.0f, 0.0f, 0.0f);
-    uint32_t node = 0;
-    float best = 0.0f;
-    for (;;) {
-        bool got;
-        pool_refill(P, pool_n, priv, pn, ph == IDLE, got, cur, link, pix);
-        if (got) ph = START;
-        if (__ballot(ph != IDLE) == 0ull) break;
-        if (ph == START) { // floor and spheres (scene_intersect), then the walk from the root
-            h.t = 1e10f;
-            h.kind = HIT_NONE;
-            h.idx = 0;
-            h.u = 0.0f;
-            h.v = 0.0f;
-            h.ni = 0;
-            h.batch = 0;
-            const f3 o = cur.o, d = cur.d;
-            if (A.flags & TRT_FLAG_FLOOR) { // shader.comp:302-320
-                if (fabsf(d.y) > TRT_EPS) {
-                    float t = div_rn(-(o.y + 4.0f), d.y);
-                    if (t > TRT_EPS && t < h.t) {
-                        f3 p = add(o, muls(d, t));
-                        if (fabsf(p.x) < 10.0f && p.z < -5.0f && p.z > -30.0f) {
-                            h.t = t;
-                            h.kind = HIT_FLOOR;
-                        }
-                    }
-                }
-            }
-            if (A.flags & TRT_FLAG_SPHERES) { // shader.comp:322-335
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float t = 1e10f;
-                    if (sphere_hit(o, d, A.sph[i], t) && t < h.t) {
-                        h.t = t;
-                        h.kind = HIT_SPHERE;
-                        h.idx = i;
-                    }
-                }
-            }
-            if (A.nbatch == 0 || ray_misses_all_batches(o, d)) {
-                ph = DONE;
-            } else {
-                inv = cull_inv(d);
-                node = 0u;
-                best = h.t;
-                stack.sp = 0;
-                ph = TRAV;
-            }
-        }
-        for (;;) { // walk steps
-            const uint64_t tm = __ballot(ph == TRAV);
-            if (tm == 0ull) break;
-            if ((uint32_t)__popcll(tm) < (uint32_t)TRT_REFILL_T && __ballot(ph == DONE) != 0ull) break;
-            if (ph == TRAV) {
-                bool more = false;
-                if (!(node & kBvhLeafBit)) {
-                    float4 pe;
-                    uint4 qa, qb, ch;
-                    const uint32_t n0 = __builtin_amdgcn_readfirstlane(node);
-                    if (__ballot(node != n0) == 0ull) { // every walking lane on one node: scalar loads
-                        typedef __attribute__((address_space(4))) const float cfloat;
-                        typedef __attribute__((address_space(4))) const uint32_t cuint;
-                        const cfloat* R = (const cfloat*)(A.bvh4q + n0);
-                        const cuint* RC = (const cuint*)(A.bvh4q + n0);
-                        pe = make_float4(R[0], R[1], R[2], R[3]);
-                        qa = make_uint4(RC[4], RC[5], RC[6], RC[7]);
-                        qb = make_uint4(RC[8], RC[9], RC[10], RC[11]);
-                        ch = make_uint4(RC[12], RC[13], RC[14], RC[15]);
-                    } else {
-                        const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
-                        pe = p[0];
-                        qa = reinterpret_cast<const uint4*>(p)[1];
-                        qb = reinterpret_cast<const uint4*>(p)[2];
-                        ch = reinterpret_cast<const uint4*>(p)[3];
-                    }
-                    more = visit4q<false>(cur.o, inv, best, pe, qa, qb, ch, stack, node, cnt);
-                } else {
-                    bvh_leaf<false, false>(A, node, cur.o, cur.d, inv, h, 0.0f, best, cnt);
-                }
-                if (!more) {
-                    if (stack.sp == 0) ph = DONE;
-                    else node = stack.pop();
-                }
-            }
-        }
-        const uint64_t dm = __ballot(ph == DONE);
-        if (dm != 0ull) { // shade the finished lanes together (one event row)
-            const uint32_t slot = ev_alloc(A, L);
-            bool have_other = false;
-            PSeg other;
-            if (ph == DONE) {
-                bool cont;
-                defer_shade<SPLIT>(A, L, slot, h, cur, link, pix, cont, other, have_other);
-                ph = cont ? START : IDLE;
-            }
-            pool_offer(P, pool_n, priv, pn, have_other, other);
-        }
     }
 }
 
@@ -2661,12 +2162,6 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
         static_assert(kDeferStripes == 128u, "stripe hash yields 7 bits");
         const size_t o = valid ? (size_t)k * A.width + x : 0u;
         const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
-        if constexpr (defer_refill<GEOM>()) {
-            if (defer_use_q(A)) {
-                defer_walk_q<SPLIT>(A, lds, slab, L, valid, root, kEvRoot, (uint32_t)o);
-                return;
-            }
-        }
         defer_walk<GEOM, SPLIT>(A, lds, slab, L, valid, root, kEvRoot, (uint32_t)o);
         return;
     }
@@ -2862,92 +2357,9 @@ __device__ __forceinline__ void flush_counts(const KArgs& A, const Cnt& cnt) {
     }
 }
 
-// Hot-first dealing (KArgs::hot, single-frame plain launches).  A single-frame launch ends with
-// its longest waves: in a C2 frame the costliest 8x8 tiles (glass-sphere pixels with 15-segment
-// trees and an envmap gather per miss) run 19-26 us against a 4.6 us median, and started at a
-// random point of the dispatch they leave the frame 30 us long against 13 us of total work /
-// slots (tools/waveclock.py, profiles/r05t_clock_c2_single_frame.log).  Neighbouring frames are
-// nearly the same, so each wave times its tile (s_memrealtime) and the tiles within 2x of the
-// previous frame's longest go into a list that the slot's next frame deals first (blocks
-// [0, hot_max)); the normal blocks skip the listed tiles.  Each tile is traced exactly once
-// either way, so the image does not depend on the lists (they only order the dispatch).
-// Measured and rejected (round 5, profiles/r05u_ab_hot_first.jsonl, r05x_ab_hot_first_*.jsonl):
-// with the lists dealt, a C2 frame at one launch per frame takes 100-120 us instead of 31 (2 in
-// flight: 72 vs 16 us), whatever the list length (8, 32, 128 or 512 tiles); recording alone
-// (lists written, not dealt) and dealing alone (extra blocks, plain order) cost 2-3 %.  The
-// runtime switch (trt_ctx::hot_first, TRT_HOT_FIRST=1) is off by default; this macro compiles
-// the path in for the tests (tests/test_gpu_hot.py: bit-identical frames).
-#ifndef TRT_HOT_FIRST
-#define TRT_HOT_FIRST 1
-#endif
-// Block vb's tile, or ~0u when the block has nothing to trace (a spare hot block, or a tile a
-// hot block traces).  The block with vb == hot_max clears the list the slot's next frame writes.
-// TRT_HOT_DIAG (diagnostic builds): 1 = no recording (the lists stay empty), 2 = recording but
-// plain dealing (the lists are not read)
-#ifndef TRT_HOT_DIAG
-#define TRT_HOT_DIAG 0
-#endif
-__device__ __forceinline__ uint32_t hot_tile(const KArgs& A, uint32_t vb) {
-    const uint32_t L = A.hot_max + 2u, k = A.hot_k % 3u;
-    const uint32_t* rd = A.hot + k * L;
-    if (TRT_HOT_DIAG == 2) return vb < A.hot_max ? ~0u : xcd_tile(A, vb - A.hot_max);
-    if (vb < A.hot_max) return vb < min(rd[0], A.hot_max) ? rd[2u + vb] : ~0u;
-    if (vb == A.hot_max && lane_id() == 0u) {
-        uint32_t* z = A.hot + ((k + 2u) % 3u) * L;
-        z[0] = 0u;
-        z[1] = 0u;
-    }
-    const uint32_t tile = xcd_tile(A, vb - A.hot_max);
-    const uint8_t* rflag = A.hot_flag + (size_t)k * A.hot_fstride;
-    return (tile >= A.ntiles || rflag[tile]) ? ~0u : tile;
-}
-// After the tile: its wave's duration dt (10-ns ticks) against the previous frame's longest; a
-// tile within 2x of it goes into the list the slot's next frame deals first.
-__device__ __forceinline__ void hot_record(const KArgs& A, uint32_t tile, uint32_t dt) {
-    if (TRT_HOT_DIAG == 1 || lane_id() != 0u) return;
-    const uint32_t L = A.hot_max + 2u, k = A.hot_k % 3u, kw = (k + 1u) % 3u;
-    const uint32_t longest = A.hot[k * L + 1u];
-    uint32_t* wr = A.hot + kw * L;
-    // (the count is read first: once the list is full, no wave touches the contended counter)
-    bool hot = longest != 0u && 2u * dt >= longest &&
-               __hip_atomic_load(&wr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A.hot_max;
-    if (hot) {
-        const uint32_t s = __hip_atomic_fetch_add(&wr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (s < A.hot_max) wr[2u + s] = tile;
-        else hot = false;
-    }
-    A.hot_flag[(size_t)kw * A.hot_fstride + tile] = hot ? 1u : 0u;
-    // the frame's longest wave: one contended address, so only a wave longer than the value it
-    // reads updates it (a per-wave atomic max on it cost 4x the frame)
-    if (dt > __hip_atomic_load(&wr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        __hip_atomic_fetch_max(&wr[1], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int GEOM, int TOP = top_nodes<GEOM>()>
+template <int GEOM>
 constexpr int slab_float4s() {
-    return GEOM == 1 ? 64 * 3
-         : GEOM == 3 ? top_off<GEOM>() + (TRT_TOP_LDS > 0 ? 1 + 4 * TOP : 0)
-         : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
-}
-// Copies the first min(TOP, nodes) quantized nodes into the slab after the traversal stack and
-// writes their count to the header (trace_bvh4); every lane of the wave calls it.
-template <int GEOM, int TOP = top_nodes<GEOM>()>
-__device__ __forceinline__ void top_fill(const KArgs& A, float4* slab) {
-    if constexpr (GEOM == 3 && TRT_TOP_LDS > 0) {
-        lds_u32* t = (lds_u32*)reinterpret_cast<uint32_t*>(slab + top_off<GEOM>());
-        const uint32_t n = A.bvh4q ? min((uint32_t)TOP, A.bvh4q_n) : 0u;
-        if (lane_id() == 0u) t[0] = n;
-        const uint4* src = reinterpret_cast<const uint4*>(A.bvh4q);
-        for (uint32_t i = lane_id(); i < n * 4u; i += 64u) {
-            const uint4 v = src[i];
-            lds_u32* d = t + 4u * (1u + i);
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
-        }
-        wave_lds_sync();
-    }
+    return GEOM == 1 ? 64 * 3 : GEOM >= 2 ? (bvh_lds_entries<GEOM>() > 0 ? bvh_lds_entries<GEOM>() * 16 : 1) : 1;
 }
 // Triangle-free frames (GEOM 0: C1 / C2) are latency-bound on the dependent chain intersection
 // -> shading -> envmap gather; 5 waves per SIMD (<= 96 VGPRs) hide more of it than the 4 the
@@ -2972,71 +2384,20 @@ constexpr int trace_waves() {
 }
 
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
-__global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void trace_kernel(KArgs A) {
-#if TRT_WPB > 1
-    // TRT_WPB waves per workgroup, each with its own LDS columns and tile; virtual block
-    // v = (b / 8) * 8 * WPB + w * 8 + b % 8 keeps every wave of block b on block b's XCD.
-    __shared__ float lds_all[(DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>()) * TRT_WPB];
-    __shared__ float4 slab_all[slab_float4s<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>() * TRT_WPB];
-    const uint32_t w = threadIdx.x >> 6;
-    float* lds = lds_all + w * (DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>());
-    float4* slab = slab_all + w * slab_float4s<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>();
-    const uint32_t vb = (blockIdx.x / 8u) * 8u * TRT_WPB + w * 8u + blockIdx.x % 8u;
-    // virtual blocks of the launch: ntiles per frame, or per frame pair (multi-frame launches)
-    const uint32_t nvb = A.ntiles * ((!SPLIT && !DEFER && A.nframes > 1u)
-                                         ? (A.xcd_inter && A.frame_group > 1u && (GEOM == 0 || TRT_MESH_PAIRS)
-                                                ? (A.nframes + 1u) / 2u : A.nframes)
-                                         : 1u);
-    if (vb >= nvb) return;
-#else
+__global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void trace_kernel(KArgs A) {
     __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, HYB>()];
     // GEOM 1: one batch slab, 64 x (v0, e1, e2); GEOM 2: the BVH traversal stacks
-    __shared__ float4 slab[slab_float4s<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>()];
+    __shared__ float4 slab[slab_float4s<GEOM>()];
     const uint32_t vb = blockIdx.x;
-#endif
-    top_fill<GEOM, (SPLIT ? 0 : top_nodes<GEOM, DEFER>())>(A, slab);
     Cnt cnt;
 #ifdef TRT_DIAG_WAVE_CLOCK
     // diagnostic: per-workgroup (tile | xcc << 28, start lo, duration, start hi) of the
     // 100 MHz constant clock, written to out32 (tools/waveclock.py)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-#if defined(TRT_PERSIST)
-    // experiment: persistent waves (grid = a whole GPU's worth); a wave of XCD x = block % 8
-    // takes TRT_PERSIST tiles at a time from its XCD's ticket counter, in xcd_tile order (its
-    // tiles are xcd_tile(j * 8 + x)); the last wave of the XCD to finish resets the counters
-    // for the slot's next frame.  Every wave leaves once the tickets pass the XCD's tiles.
-    {
-        const uint32_t xc = blockIdx.x % 8u;
-        const uint32_t per = A.ntiles > xc ? (A.ntiles - xc + 7u) / 8u : 0u;
-        uint32_t* t = A.persist + xc * 32u;
-        for (;;) {
-            uint32_t j0 = 0;
-            if (lane_id() == 0) j0 = atomicAdd(t, (uint32_t)TRT_PERSIST);
-            j0 = __shfl(j0, 0, 64);
-            if (j0 >= per) break;
-            const uint32_t j1 = min(j0 + (uint32_t)TRT_PERSIST, per);
-            for (uint32_t j = j0; j < j1; ++j) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[0], xcd_tile(A, j * 8u + xc), cnt, lds, slab);
-        }
-        if (lane_id() == 0) {
-            const uint32_t nw = (gridDim.x - xc + 7u) / 8u;
-            if (atomicAdd(t + 16, 1u) == nw - 1u) {
-                atomicExch(t, 0u);
-                atomicExch(t + 16, 0u);
-            }
-        }
-    }
-#elif defined(TRT_TPW)
-    // diagnostic: TRT_TPW tiles per wave, grid-strided (b, b + G, ...; G % 8 == 0 keeps XCDs)
-    for (uint32_t k = 0; k < TRT_TPW; ++k) {
-        const uint32_t b = blockIdx.x + k * gridDim.x;
-        if (b < A.ntiles) trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[0], xcd_tile(A, b), cnt, lds, slab);
-    }
-#else
     // frame f = vb / ntiles of a multi-frame launch (plain frames only: split / deferred frames
     // and counting passes launch one frame)
     uint32_t f = 0, t = vb, tile;
-    bool hot = false; // wave-uniform: this block was dealt by hot_tile
     if (!SPLIT && !DEFER && A.spp_lanes) { // one lane per sample: ntiles * spp waves per frame
         const uint32_t per = A.ntiles * A.spp;
         f = vb / per;
@@ -3072,33 +2433,10 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
         tile = xcd_tile(A, t / A.defer_sub);
         trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % A.defer_sub);
         return;
-    } else if (!COUNT && !SPLIT && !DEFER && TRT_HOT_FIRST && TRT_WPB == 1 && A.hot_max) {
-        // hot-first dealing (one trace_tile call site with the plain path: a second inlined
-        // copy spilled the 96-VGPR kernels)
-        tile = __builtin_amdgcn_readfirstlane(hot_tile(A, vb)); // wave-uniform: keep it scalar
-        if (tile == ~0u) return;
-        hot = true;
     } else {
         tile = xcd_tile(A, t);
     }
-#if TRT_WPB == 1
-    // The tile and the start time wait in LDS (volatile: read back, not kept in registers) —
-    // values held across trace_tile cost the 96-VGPR kernels spills (SGPR spills live in VGPR
-    // lanes).  `hot` itself is re-read from the block index.
-    __shared__ volatile uint32_t hot_rec[2];
-    if (hot) {
-        hot_rec[0] = tile;
-        hot_rec[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    }
-#endif
     trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab);
-#if TRT_WPB == 1
-    if (!COUNT && !SPLIT && !DEFER && TRT_HOT_FIRST && A.hot_max && A.nframes <= 1u && !A.spp_lanes) {
-        const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        hot_record(A, hot_rec[0], t1 - hot_rec[1]);
-    }
-#endif
-#endif
 #ifdef TRT_DIAG_WAVE_CLOCK
     __syncthreads();
     // single-frame launches write the records to out32; multi-frame launches to the diagnostic
@@ -3109,11 +2447,7 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
         uint32_t* rec = reinterpret_cast<uint32_t*>(clk) + 4 * (size_t)blockIdx.x;
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-#if !defined(TRT_PERSIST) && !defined(TRT_TPW)
         rec[0] = (A.out32 ? xcd_tile(A, blockIdx.x) : (tile | (f << 20))) | ((xcc & 15u) << 28);
-#else
-        rec[0] = xcd_tile(A, blockIdx.x) | ((xcc & 15u) << 28);
-#endif
         rec[1] = (uint32_t)t_start;
         rec[2] = (uint32_t)(t_end - t_start);
         rec[3] = (uint32_t)(t_start >> 32);
@@ -3133,8 +2467,7 @@ __global__ __launch_bounds__(64 * TRT_WPB, (trace_waves<GEOM, CAP, SPLIT, DEFER>
 template <int CAP, bool COUNT, int GEOM, bool DEFER = false>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs A) {
     __shared__ float lds[DEFER ? defer_pool_floats() : lds_stack_floats<CAP, GEOM, true>()];
-    __shared__ float4 slab[slab_float4s<GEOM, 0>()];
-    top_fill<GEOM, 0>(A, slab); // split tasks: no node copy (their LDS goes to segment stacks)
+    __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
     const uint32_t n = min(*A.q_in_n, A.q_cap);
     // static schedule: wave b takes the 64-task blocks b, b + G, ... (a dequeue atomic per block
@@ -3156,12 +2489,6 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
             EvLog L;
             // wave-uniform (ev_alloc and the query appends reserve from one stripe per wave)
             L.stripe = ((base / 64u + 0x5bd1e995u * A.split_d1) * 0x9E3779B1u) >> (32 - 7);
-            if constexpr (defer_refill<GEOM>()) {
-                if (defer_use_q(A)) {
-                    defer_walk_q<true>(A, lds, slab, L, valid, root, link, pixel);
-                    continue;
-                }
-            }
             defer_walk<GEOM, true>(A, lds, slab, L, valid, root, link, pixel);
             continue;
         }
@@ -3224,98 +2551,9 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
 // lanes sit at a hit.  Static schedule: wave w takes stripe w % kDeferStripes and every
 // (gridDim / kDeferStripes)-th 64-query block of it.  An occluded query ORs its light's bit
 // into its event.
-// Pass B with the any-hit walk turned inside out (GEOM 3, as defer_walk_q): each lane takes the
-// wave's next query as soon as its walk ends (early exits on an occluder make the walks' lengths
-// differ a lot), one node visit or leaf test per step.  The answer is shadow_intersect's: any
-// accepted occluder, in any order.  Measured and rejected (round 4): the shipped frame +5 % over
-// the per-query pass B (profiles/r04d_ab_deep.jsonl); opt-in (TRT_SHADOW_REFILL).
-#ifndef TRT_SHADOW_REFILL
-#define TRT_SHADOW_REFILL 0
-#endif
-__device__ __forceinline__ void defer_shadows_q(const KArgs& A, float4* slab) {
-    const uint32_t s = blockIdx.x % kDeferStripes, K = gridDim.x / kDeferStripes, b0 = blockIdx.x / kDeferStripes;
-    const uint32_t n = min(A.dctr->nq[s * kCtrStride], A.shq_cap);
-    const float4* Q = A.shq + 2 * (size_t)s * A.shq_cap;
-    // this wave's queries: its 64-query blocks b0, b0 + K, ... in order, ticket by ticket
-    auto qidx = [&](uint32_t t) { return (b0 + (t >> 6) * K) * 64u + (t & 63u); };
-    using Stack = BvhStack<bvh_lds_entries<3>(), false>;
-    typename Stack::Mem stack_mem;
-    Stack stack(slab, stack_mem);
-    Cnt cnt;
-    Hit unused;
-    bool walking = false;
-    f3 o = mk(0.0f, 0.0f, 0.0f), d = o, inv = o;
-    float maxd = 0.0f, best = 0.0f;
-    uint32_t node = 0, tag = 0, tick = 0; // tick: wave-uniform
-    for (;;) {
-        const uint64_t idle = __ballot(!walking);
-        const bool more = qidx(tick) < n;
-        if (idle != 0ull && more) {
-            const uint32_t i = qidx(tick + lane_rank(idle));
-            if (!walking && i < n) {
-                const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
-                o = mk(a.x, a.y, a.z);
-                d = mk(b.x, b.y, b.z);
-                maxd = a.w;
-                tag = __float_as_uint(b.w);
-                bool occ = false;
-                if (A.flags & TRT_FLAG_SPHERES) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        float t = 1e10f;
-                        if (!occ && sphere_hit(o, d, A.sph[k], t) && t < maxd) occ = true;
-                    }
-                }
-                if (occ) {
-                    atomicOr(reinterpret_cast<uint32_t*>(ev_plane(A, tag >> 2, 3)) + 1, 1u << (tag & 3u));
-                } else if (!ray_misses_all_batches(o, d)) {
-                    inv = cull_inv(d);
-                    best = maxd;
-                    node = 0u;
-                    stack.sp = 0;
-                    walking = true;
-                }
-            }
-            tick += (uint32_t)__popcll(idle);
-        }
-        for (;;) { // walk steps
-            const uint64_t wm = __ballot(walking);
-            if (wm == 0ull) break;
-            if ((uint32_t)__popcll(wm) < (uint32_t)TRT_REFILL_T && qidx(tick) < n) break;
-            if (walking) {
-                bool next = false, occ = false;
-                if (!(node & kBvhLeafBit)) {
-                    const float4* p = reinterpret_cast<const float4*>(A.bvh4q + node);
-                    const float4 pe = p[0];
-                    const uint4 qa = reinterpret_cast<const uint4*>(p)[1], qb = reinterpret_cast<const uint4*>(p)[2],
-                                ch = reinterpret_cast<const uint4*>(p)[3];
-                    next = visit4q<false>(o, inv, best, pe, qa, qb, ch, stack, node, cnt);
-                } else {
-                    occ = bvh_leaf<false, true>(A, node, o, d, inv, unused, maxd, best, cnt);
-                }
-                if (occ) {
-                    atomicOr(reinterpret_cast<uint32_t*>(ev_plane(A, tag >> 2, 3)) + 1, 1u << (tag & 3u));
-                    walking = false;
-                } else if (!next) {
-                    if (stack.sp == 0) walking = false;
-                    else node = stack.pop();
-                }
-            }
-        }
-        if (__ballot(walking) == 0ull && !(qidx(tick) < n)) break;
-    }
-}
-
 template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
-    if constexpr (GEOM == 3 && TRT_SHADOW_REFILL && !TRT_BVH_COMPRESS && TRT_BVH_QUANT && TRT_BVH_WIDTH == 4) {
-        if (A.bvh4 && A.bvh4q && A.nbatch != 0) {
-            defer_shadows_q(A, slab);
-            return;
-        }
-    }
     Cnt cnt;
     const uint32_t s = blockIdx.x % kDeferStripes, K = gridDim.x / kDeferStripes;
     const uint32_t n = min(A.dctr->nq[s * kCtrStride], A.shq_cap);
@@ -3398,7 +2636,6 @@ template <int CAP, int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KArgs A) {
     __shared__ float lds[lds_stack_floats<CAP, GEOM, false>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
     Cnt cnt;
     const uint32_t n = A.dctr->nfb;
     const f3 orig = mk(A.fr[0].cam[0], A.fr[0].cam[1], A.fr[0].cam[2]);
@@ -3416,312 +2653,6 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KAr
 static uint32_t defer_stages() { // debug: TRT_DEFER_STAGES bitmask of passes to launch
     const char* e = getenv("TRT_DEFER_STAGES");
     return e ? (uint32_t)strtoul(e, nullptr, 0) : 0xFFu;
-}
-
-// ---- deferred frame, level mode (trt_device.h LevCtr) --------------------------------------
-//
-// One launch per depth of the frame's segment trees.  Each lane traces ONE segment: its closest
-// hit, its Phong terms with their shadow rays traced inline (shader.comp:483-507; a wave's lanes
-// query the same light at the same time, from neighbouring points at low depths, so the
-// wave-coherent shadow walk applies), its colour term, and its children (shader.comp:509-575),
-// which go to the next level's queue.  Why: in the pool design (defer_walk) a tile's wave
-// carried every segment of its 64 pixels' trees, so a glass tile ran for its deepest pixel's
-// chain while other tiles idled, and the frame's latency was its slowest tile; here every
-// launch spreads one depth's segments of the whole frame over the GPU in full waves.
-#ifndef TRT_LV_WAVES
-#define TRT_LV_WAVES 4
-#endif
-#ifndef TRT_LV_WPC
-#define TRT_LV_WPC 8 /* level_kernel grid: workgroups (one wave each) per CU */
-#endif
-
-// The pixel goes to defer_fallback (once): a child that did not fit the level queue or the
-// event slots.
-__device__ __forceinline__ void lv_mark(const KArgs& A, uint32_t pix) {
-    if (atomicExch(&A.lv_flag[pix], 1u) == 0u) A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
-}
-
-// One segment of level `lvl`: closest hit, colour term with inline shadow rays, children.  Every
-// lane of the wave calls it (the child append is wave-aggregated); `valid` lanes hold a segment.
-// `slot`: its event slot; `nbase`: the first event slot of level lvl + 1.
-template <int GEOM>
-__device__ __forceinline__ void lv_segment(const KArgs& A, bool valid, Seg cur, uint32_t pix, uint32_t slot,
-                                           uint32_t lvl, uint32_t nbase, float4* slab) {
-    Cnt cnt;
-    f3 term = mk(0.0f, 0.0f, 0.0f);
-    bool mk_refl = false, mk_refr = false;
-    Seg refl, refr;
-    if (valid) {
-        Hit h;
-        scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
-        if (h.kind == HIT_NONE) {
-            term = muls(background(A, cur.d), cur.thr); // shader.comp:455-458
-        } else {
-            const Surf sf = resolve_hit<false>(A, cur, h, cnt);
-            const f3 v = neg(cur.d);
-            const f3 kdv = mk(sf.kd[0], sf.kd[1], sf.kd[2]);
-            f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) { // shader.comp:491-505
-                const LightTerm t = light_term(A, sf, v, i);
-                if (!t.matters) continue;
-                if (shadow_intersect<false, GEOM>(A, t.so, t.ld, t.dist, cnt, slab)) continue;
-                diffuse = add(diffuse, muls(kdv, t.diff));
-                specular = add(specular, muls(kdv, t.spec));
-            }
-            term = muls(add(muls(diffuse, sf.alb[0]), muls(specular, sf.alb[1])), cur.thr);
-            make_children(cur, sf, (int)A.max_depth, refr, mk_refr, refl, mk_refl);
-        }
-    }
-    // children to level lvl + 1: the wave's reflection children, then its refraction children
-    uint32_t srefl = kEvNone, srefr = kEvNone;
-    const uint64_t ba = __ballot(mk_refl), bb = __ballot(mk_refr);
-    if ((ba | bb) != 0ull) {
-        const uint32_t na = (uint32_t)__popcll(ba), nb = (uint32_t)__popcll(bb);
-        uint32_t q0 = 0;
-        if (lane_id() == 0u) q0 = atomicAdd(&A.lv_ctr->n[(lvl + 1u) * kCtrStride], na + nb);
-        q0 = __shfl(q0, 0, 64);
-        float4* Q = A.lv_q[(lvl + 1u) & 1u];
-        bool ovf = false;
-        auto put = [&](bool f, uint32_t i, const Seg& x, uint32_t& sl) {
-            if (!f) return;
-            if (i >= A.lv_qcap || nbase + i >= A.lv_evcap) {
-                ovf = true;
-                return;
-            }
-            Q[2 * (size_t)i] = make_float4(x.o.x, x.o.y, x.o.z, x.d.x);
-            Q[2 * (size_t)i + 1] = make_float4(x.d.y, x.d.z, x.thr, __uint_as_float(pix));
-            sl = nbase + i;
-        };
-        put(mk_refl, q0 + lane_rank(ba), refl, srefl);
-        put(mk_refr, q0 + na + lane_rank(bb), refr, srefr);
-        if (ovf) lv_mark(A, pix);
-    }
-    if (valid) {
-        A.lv_ev[slot] = make_float4(term.x, term.y, term.z, __uint_as_float(srefl));
-        A.lv_evr[slot] = srefr;
-    }
-}
-
-// Entries of a level queue that were written: a parent queues a child only when its entry
-// index fits the queue and its event slot fits the event slots (lv_segment), so of the n
-// requested entries of a level whose first event slot is `base`, min(n, qcap, evcap - base)
-// exist.  Level k's base is npx plus the earlier levels' written entries.
-__device__ __forceinline__ uint32_t lv_written(const KArgs& A, uint32_t n, uint32_t base) {
-    n = min(n, A.lv_qcap);
-    return base >= A.lv_evcap ? 0u : min(n, A.lv_evcap - base);
-}
-// (level lvl's written entries, its first event slot)
-__device__ __forceinline__ uint2 lv_level_range(const KArgs& A, uint32_t lvl) {
-    const LevCtr* C = A.lv_ctr;
-    uint32_t base = A.rows * A.width;
-    for (uint32_t j = 1u; j < lvl; ++j) base += lv_written(A, C->n[j * kCtrStride], base);
-    return make_uint2(lv_written(A, C->n[lvl * kCtrStride], base), base);
-}
-
-// Level 0: the primary rays, one 8x8 tile per wave (xcd_tile dealing, as trace_kernel).
-template <int GEOM>
-__global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level0(KArgs A) {
-    __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
-    const uint32_t tile = xcd_tile(A, blockIdx.x), lane = lane_id();
-    if (tile >= A.ntiles) return;
-    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
-    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
-    const bool valid = x < A.width && k < A.rows;
-    const FrameRec& F = A.fr[0];
-    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
-    const uint32_t o = valid ? k * A.width + x : 0u;
-    const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
-    lv_segment<GEOM>(A, valid, root, o, o, 0u, A.rows * A.width, slab);
-}
-
-// Level lvl >= 1: waves take 64-entry chunks of the level's queue until it is drained.
-template <int GEOM>
-__global__ __launch_bounds__(64, TRT_LV_WAVES) void lv_level(KArgs A) {
-    __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
-    const uint32_t lvl = A.lv_level;
-    const uint2 nb = lv_level_range(A, lvl);
-    const uint32_t n = nb.x, base = nb.y; // written entries, first event slot of this level
-    if (n == 0u) return;
-    const float4* Q = A.lv_q[lvl & 1u];
-    for (;;) {
-        uint32_t c = 0;
-        if (lane_id() == 0u) c = atomicAdd(&A.lv_ctr->take[lvl * kCtrStride], 1u);
-        c = __shfl(c, 0, 64);
-        if (c * 64u >= n) break;
-        const uint32_t i = c * 64u + lane_id();
-        const bool valid = i < n;
-        Seg cur{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f), 0.0f, (int)lvl};
-        uint32_t pix = 0;
-        if (valid) {
-            const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
-            cur.o = mk(a.x, a.y, a.z);
-            cur.d = mk(a.w, b.x, b.y);
-            cur.thr = b.z;
-            pix = __float_as_uint(b.w);
-        }
-        lv_segment<GEOM>(A, valid, cur, pix, base + i, lvl, base + n, slab);
-    }
-}
-
-// Level mode 2: the same levels with the shadow rays deferred to pass B (defer_shadows) and the
-// pool design's events (defer_shade: kd, terms and weights, 64 B) at implicit slots, so a
-// level's critical path is its closest-hit walks only.  A segment's children go to the next
-// level's queue with their parent links; defer_shade links each event into its parent's.
-template <int GEOM>
-__device__ __forceinline__ void lvb_segment(const KArgs& A, bool valid, Seg cur, uint32_t pix, uint32_t link,
-                                            uint32_t slot, uint32_t lvl, uint32_t nbase, uint32_t stripe,
-                                            float4* slab) {
-    Cnt cnt;
-    bool have = false, have_other = false;
-    PSeg other;
-    EvLog L;
-    L.stripe = stripe;
-    if (valid) {
-        Hit h;
-        scene_intersect<false, GEOM>(A, cur.o, cur.d, h, cnt, slab);
-        defer_shade<false>(A, L, slot, h, cur, link, pix, have, other, have_other);
-    }
-    // children to level lvl + 1 (defer_shade left the first in cur / link, the second in other)
-    const uint64_t ba = __ballot(have), bb = __ballot(have_other);
-    if ((ba | bb) != 0ull) {
-        const uint32_t na = (uint32_t)__popcll(ba), nb = (uint32_t)__popcll(bb);
-        uint32_t q0 = 0;
-        if (lane_id() == 0u) q0 = atomicAdd(&A.lv_ctr->n[(lvl + 1u) * kCtrStride], na + nb);
-        q0 = __shfl(q0, 0, 64);
-        float4* Q = A.lv_q[(lvl + 1u) & 1u];
-        uint32_t* QL = A.lv_qlink[(lvl + 1u) & 1u];
-        bool ovf = false;
-        auto put = [&](bool f, uint32_t i, const Seg& x, uint32_t lk) {
-            if (!f) return;
-            if (i >= A.lv_qcap || nbase + i >= A.lv_evcap) {
-                ovf = true;
-                return;
-            }
-            Q[2 * (size_t)i] = make_float4(x.o.x, x.o.y, x.o.z, x.d.x);
-            Q[2 * (size_t)i + 1] = make_float4(x.d.y, x.d.z, x.thr, __uint_as_float(pix));
-            QL[i] = lk;
-        };
-        put(have, q0 + lane_rank(ba), cur, link);
-        put(have_other, q0 + na + lane_rank(bb), other.s, other.link);
-        if (ovf) defer_mark_fallback(A, pix);
-    }
-}
-
-template <int GEOM>
-__global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level0(KArgs A) {
-    __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
-    const uint32_t tile = xcd_tile(A, blockIdx.x), lane = lane_id();
-    if (tile >= A.ntiles) return;
-    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
-    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
-    const bool valid = x < A.width && k < A.rows;
-    const FrameRec& F = A.fr[0];
-    const f3 orig = mk(F.cam[0], F.cam[1], F.cam[2]);
-    const uint32_t o = valid ? k * A.width + x : 0u;
-    const Seg root = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
-    const uint32_t stripe = (tile * 0x9E3779B1u) >> (32 - 7);
-    lvb_segment<GEOM>(A, valid, root, o, kEvRoot, o, 0u, A.rows * A.width, stripe, slab);
-}
-
-template <int GEOM>
-__global__ __launch_bounds__(64, TRT_LV_WAVES) void lvb_level(KArgs A) {
-    __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
-    const uint32_t lvl = A.lv_level;
-    const uint2 nb = lv_level_range(A, lvl);
-    const uint32_t n = nb.x, base = nb.y;
-    if (n == 0u) return;
-    const float4* Q = A.lv_q[lvl & 1u];
-    const uint32_t* QL = A.lv_qlink[lvl & 1u];
-    for (;;) {
-        uint32_t c = 0;
-        if (lane_id() == 0u) c = atomicAdd(&A.lv_ctr->take[lvl * kCtrStride], 1u);
-        c = __shfl(c, 0, 64);
-        if (c * 64u >= n) break;
-        const uint32_t i = c * 64u + lane_id();
-        const bool valid = i < n;
-        Seg cur{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f), 0.0f, (int)lvl};
-        uint32_t pix = 0, link = kEvRoot;
-        if (valid) {
-            const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
-            cur.o = mk(a.x, a.y, a.z);
-            cur.d = mk(a.w, b.x, b.y);
-            cur.thr = b.z;
-            pix = __float_as_uint(b.w);
-            link = QL[i];
-        }
-        const uint32_t stripe = ((c + 0x5bd1e995u * lvl) * 0x9E3779B1u) >> (32 - 7);
-        lvb_segment<GEOM>(A, valid, cur, pix, link, base + i, lvl, base + n, stripe, slab);
-    }
-}
-
-// Pass C of a level-mode frame: each pixel's terms summed in the reference's pop order
-// (shader.comp:530-575), then clamp, gamma and the dual store.  Pixels handed to the fallback
-// are skipped.
-__global__ __launch_bounds__(64) void lv_resolve(KArgs A) {
-    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
-    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
-    const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
-    if (x >= A.width || k >= A.rows) return;
-    const uint32_t o = k * A.width + x;
-    if (A.lv_flag[o]) return;
-    f3 color = mk(0.0f, 0.0f, 0.0f);
-    uint32_t stk[kMaxTreeDepth]; // pending refraction subtrees, one per depth of the path
-    uint32_t s = o, sp = 0, steps = 0;
-    for (;;) {
-        // a tree has at most 2^MAX_DEPTH - 1 events: a corrupt log must not hang the GPU
-        if (++steps > (1u << kMaxTreeDepth) || s >= A.lv_evcap) {
-            color = mk(1.0f, 0.0f, 1.0f);
-            break;
-        }
-        const float4 e = A.lv_ev[s];
-        color = add(color, mk(e.x, e.y, e.z));
-        const uint32_t refl = __float_as_uint(e.w), refr = A.lv_evr[s];
-        if (refl != kEvNone) {
-            if (refr != kEvNone && sp < kMaxTreeDepth) stk[sp++] = refr;
-            s = refl;
-        } else if (refr != kEvNone) {
-            s = refr;
-        } else if (sp > 0u) {
-            s = stk[--sp];
-        } else {
-            break;
-        }
-    }
-    store_pixel(A, A.fr[0], o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
-}
-
-template <int CAP, int GEOM>
-static void launch_levels(const KArgs& A0, hipStream_t stream, dim3 grid) {
-    KArgs A = A0;
-    const uint32_t stages = defer_stages();
-    if (A.lv == 2) { // shadow rays deferred: the levels, then passes B and C of the pool design
-        if (stages & 1) hipLaunchKernelGGL(lvb_level0<GEOM>, grid, dim3(64), 0, stream, A);
-        for (uint32_t k = 1; k < A.max_depth && (stages & 2); ++k) {
-            A.lv_level = k;
-            hipLaunchKernelGGL(lvb_level<GEOM>, dim3(A.num_cus * TRT_LV_WPC), dim3(64), 0, stream, A);
-        }
-        if (stages & 4)
-            hipLaunchKernelGGL(defer_shadows<GEOM>,
-                               dim3(((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes), dim3(64), 0,
-                               stream, A);
-        if (stages & 8) hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
-        if (stages & 16)
-            hipLaunchKernelGGL((defer_fallback<CAP, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
-        return;
-    }
-    if (stages & 1) hipLaunchKernelGGL(lv_level0<GEOM>, grid, dim3(64), 0, stream, A);
-    for (uint32_t k = 1; k < A.max_depth && (stages & 2); ++k) {
-        A.lv_level = k;
-        hipLaunchKernelGGL(lv_level<GEOM>, dim3(A.num_cus * TRT_LV_WPC), dim3(64), 0, stream, A);
-    }
-    if (stages & 8) hipLaunchKernelGGL(lv_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
-    if (stages & 16)
-        hipLaunchKernelGGL((defer_fallback<CAP, GEOM>), dim3(A.num_cus), dim3(64), 0, stream, A);
 }
 
 
@@ -3779,7 +2710,6 @@ template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void shadow_batch_kernel(KArgs A, const float4* __restrict__ rays,
                                                                                 uint32_t n, uint32_t* __restrict__ occ) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
-    top_fill<GEOM>(A, slab);
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n) return;
     const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];
@@ -3815,31 +2745,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool) {
 #else
 hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const uint32_t D = A.max_depth;
-#if defined(TRT_PERSIST)
-    // experiment: one GPU's worth of waves (TRT_PERSIST_WPC waves per CU)
-    const dim3 grid(A.num_cus * TRT_PERSIST_WPC), block(64);
-#elif defined(TRT_TPW)
-    const dim3 grid((A.ntiles + TRT_TPW - 1) / TRT_TPW), block(64);
-#elif TRT_WPB > 1
-    const dim3 grid(((A.ntiles + 8 * TRT_WPB - 1) / (8 * TRT_WPB)) * 8), block(64 * TRT_WPB);
-#else
     const dim3 grid(A.ntiles), block(64);
-#endif
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
-    if (A.defer && A.lv && !count && A.spp <= 1 && A.dctr && A.fb && A.lv_q[0] && A.lv_q[1] && A.lv_ctr &&
-        (A.lv == 2 ? (A.ev && A.shq && A.px_ev && A.lv_qlink[0] && A.lv_qlink[1]) : (A.lv_ev && A.lv_evr && A.lv_flag))) {
-        // level mode: memsets of the counters (and the inline design's fallback flags), then the levels
-        hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
-        if (e == hipSuccess) e = hipMemsetAsync(A.lv_ctr, 0, sizeof(LevCtr), stream);
-        if (e == hipSuccess && A.lv == 1) e = hipMemsetAsync(A.lv_flag, 0, (size_t)A.rows * A.width * sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-        // the fallback runs the per-pixel loop with the full-depth private stack
-        if (geom == 0) launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 0>(A, stream, grid);
-        else if (geom == 1) launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 1>(A, stream, grid);
-        else if (geom == 2) launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 2>(A, stream, grid);
-        else launch_levels<(int)TRT_MAX_DEPTH_LIMIT - 1, 3>(A, stream, grid);
-        return hipGetLastError();
-    }
     if (A.defer && !count && A.spp <= 1 && A.dctr && A.ev && A.shq && A.px_ev && A.fb) {
         hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
         if (e == hipSuccess && A.split_w >= 1 && A.ctr) e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
@@ -3886,20 +2793,11 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
         return hipGetLastError();
     }
     // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)
-#if !defined(TRT_PERSIST) && !defined(TRT_TPW)
     const uint32_t fblocks = A.spp_lanes ? std::max(A.nframes, 1u) * A.spp
                              : A.nframes > 1u && A.xcd_inter && A.frame_group > 1u && (geom == 0 || TRT_MESH_PAIRS)
                                  ? (A.nframes + 1u) / 2u
                                  : std::max(A.nframes, 1u);
-#if TRT_WPB == 1
-    // hot-first dealing (trace_hot): hot_max extra blocks ahead of the frame's tiles
-    const dim3 fgrid(A.ntiles * fblocks + (!count && TRT_HOT_FIRST && fblocks == 1u && A.nframes <= 1u && !A.spp_lanes ? A.hot_max : 0u));
-#else // TRT_WPB waves per workgroup: virtual blocks as in trace_kernel, whole groups of 8 blocks
-    const dim3 fgrid(((A.ntiles * fblocks + 8 * TRT_WPB - 1) / (8 * TRT_WPB)) * 8);
-#endif
-#else
-    const dim3 fgrid = grid;
-#endif
+    const dim3 fgrid(A.ntiles * fblocks);
 #define TRT_LAUNCH_G(CAP, G)                                                                             \
     do {                                                                                                 \
         if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G, false>), fgrid, block, 0, stream, A);  \

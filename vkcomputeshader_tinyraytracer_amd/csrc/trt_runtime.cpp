@@ -39,9 +39,8 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count);
 hipError_t launch_envp(const uint32_t* env, uint2* out, uint32_t W, uint32_t H, hipStream_t stream);
 hipError_t launch_shadow_batch(const KArgs& A, const float4* rays, uint32_t n, uint32_t* occ, hipStream_t stream);
 uint32_t collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4);
+uint32_t bvh_depth(const std::vector<BvhNode>& b2);
 bool quantize_bvh4(const std::vector<Bvh4Node>& b4, std::vector<Bvh4QNode>& out);
-bool compress_bvh4(std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4, const std::vector<Bvh4QNode>& q,
-                   std::vector<TriGeo>& leaf_tris, std::vector<Bvh4CNode>& out);
 bool build_bvh(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                std::vector<BvhNode>& nodes, std::vector<TriGeo>& leaf_tris);
 }
@@ -61,7 +60,18 @@ int fail(trt_ctx* c, int code, const std::string& msg) {
 }
 
 int hip_fail(trt_ctx* c, hipError_t e, const char* what) {
-    return fail(c, TRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    // an allocation failure is reported through the return code; its sticky last-error state
+    // must not surface in the caller's next HIP call (a torch launch check)
+    if (e == hipErrorOutOfMemory) (void)hipGetLastError();
+    return fail(c, e == hipErrorOutOfMemory ? TRT_ERR_OOM : TRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Failure injection (tests only, with TRT_ENABLE_TEST_HOOKS=1): TRT_TEST_FAIL_DEFER_SLOT=k makes
+// the deferred-frame scratch allocation of in-flight slot k report out-of-memory.
+int test_fail_defer_slot() {
+    const char* on = std::getenv("TRT_ENABLE_TEST_HOOKS");
+    const char* e = std::getenv("TRT_TEST_FAIL_DEFER_SLOT");
+    return (on && std::atoi(on) == 1 && e) ? std::atoi(e) : -1;
 }
 
 #define HIP_TRY(ctx, expr)                                       \
@@ -76,7 +86,6 @@ void free_scene(trt_ctx* c) {
     (void)hipFree(c->d_bvh);
     (void)hipFree(c->d_bvh4);
     (void)hipFree(c->d_bvh4q);
-    (void)hipFree(c->d_bvh4c);
     (void)hipFree(c->d_bvh_tris);
     (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade);
@@ -87,7 +96,6 @@ void free_scene(trt_ctx* c) {
     c->d_bvh = nullptr;
     c->d_bvh4 = nullptr;
     c->d_bvh4q = nullptr;
-    c->d_bvh4c = nullptr;
     c->d_bvh_tris = nullptr;
     c->top = 0;
     c->d_geo = nullptr;
@@ -129,11 +137,6 @@ Mat to_mat(const trt_material& m) {
 // TRT_BVH_COMPRESS: 0 = no 48-B nodes (default: measured slower), 1 = for
 // the 4-wave BVH build, 2 = every BVH4 walk; the kernel walks them only when built with
 // -DTRT_BVH_COMPRESS=1.  Read at every scene upload / frame.
-int bvh_compress_mode() {
-    const char* e = std::getenv("TRT_BVH_COMPRESS");
-    return e ? std::atoi(e) : 0;
-}
-
 void fill_ubo_args(KArgs& A, const trt_ubo& u) {
     const trt_sphere* s[4] = {&u.sphere0, &u.sphere1, &u.sphere2, &u.sphere3};
     for (int i = 0; i < 4; ++i) {
@@ -207,9 +210,7 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (hipSetDevice(hip_device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counters, 32 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&c->d_persist, kPersistWords * TRT_BUILD_MAX_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(c->d_persist, 0, kPersistWords * TRT_BUILD_MAX_IN_FLIGHT * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc((void**)&c->d_counters, 32 * sizeof(unsigned long long)) != hipSuccess) {
         trt_destroy(c);
         return TRT_ERR_HIP;
     }
@@ -222,11 +223,7 @@ int trt_create(trt_ctx** out, int hip_device) {
         return TRT_ERR_HIP;
     }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
-    if (const char* e = std::getenv("TRT_DEFER_MODE"))
-        c->defer_design = std::strcmp(e, "levels") == 0 ? TRT_DEFER_LEVELS
-                          : std::strcmp(e, "levels_b") == 0 ? TRT_DEFER_LEVELS_B : TRT_DEFER_POOL;
     if (const char* e = std::getenv("TRT_SPP_LANES")) c->spp_lanes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("TRT_HOT_FIRST")) c->hot_first = std::atoi(e) != 0;
     if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32 or 16
         const int ppw = std::atoi(e);
         c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
@@ -255,7 +252,6 @@ int trt_destroy(trt_ctx* c) {
     (void)hipFree(c->d_out32);
     (void)hipFree(c->d_rays);
     (void)hipFree(c->d_counters);
-    (void)hipFree(c->d_persist);
     for (hipEvent_t e : c->fev) (void)hipEventDestroy(e);
     for (auto& b : c->split) {
         (void)hipFree(b.q[0]);
@@ -270,8 +266,6 @@ int trt_destroy(trt_ctx* c) {
         (void)hipFree(b.px_ev);
         (void)hipFree(b.fb);
         (void)hipFree(b.dctr);
-        (void)hipFree(b.hot);
-        (void)hipFree(b.hot_flag);
         if (b.done) (void)hipEventDestroy(b.done);
     }
     for (hipStream_t s : c->aux) {
@@ -319,15 +313,6 @@ int trt_set_deferred_shadows(trt_ctx* c, int mode) {
     return TRT_OK;
 }
 
-int trt_set_defer_design(trt_ctx* c, int design) {
-    if (!c) return TRT_ERR_INVALID;
-    if (design != TRT_DEFER_POOL && design != TRT_DEFER_LEVELS && design != TRT_DEFER_LEVELS_B)
-        return fail(c, TRT_ERR_INVALID,
-                    "trt_set_defer_design: design must be TRT_DEFER_POOL, TRT_DEFER_LEVELS or TRT_DEFER_LEVELS_B");
-    c->defer_design = design;
-    return TRT_OK;
-}
-
 int trt_defer_stats(trt_ctx* c, uint32_t slot, uint64_t out[5]) {
     if (!c || !out) return TRT_ERR_INVALID;
     if (slot >= TRT_BUILD_MAX_IN_FLIGHT) return fail(c, TRT_ERR_INVALID, "trt_defer_stats: slot out of range");
@@ -339,26 +324,10 @@ int trt_defer_stats(trt_ctx* c, uint32_t slot, uint64_t out[5]) {
     if (b.last && b.done) HIP_TRY(c, hipEventSynchronize(b.done));
     trt::DeferCtr d{};
     HIP_TRY(c, hipMemcpy(&d, b.dctr, sizeof(d), hipMemcpyDeviceToHost));
-    if (b.last_levels) { // the slot's last deferred frame ran the level design
-        trt::LevCtr lc{};
-        HIP_TRY(c, hipMemcpy(&lc, b.lv_ctr, sizeof(lc), hipMemcpyDeviceToHost));
-        uint64_t ev = b.last_npx, big = 0; // written entries as the kernel counts them (lv_written)
-        for (uint32_t k = 1; k <= trt::kMaxTreeDepth; ++k) {
-            const uint64_t n = lc.n[k * trt::kCtrStride];
-            const uint64_t w = ev >= b.lv_evcap ? 0 : std::min<uint64_t>(std::min<uint64_t>(n, b.lv_qcap), b.lv_evcap - ev);
-            ev += w;
-            big = std::max<uint64_t>(big, n);
-            if (std::getenv("TRT_LV_DEBUG")) std::fprintf(stderr, "trt: level %u: %llu entries\n", k, (unsigned long long)n);
-        }
-        out[0] = ev;
-        out[1] = big;
-        out[2] = d.nfb;
-        out[3] = b.lv_evcap;
-        out[4] = b.lv_qcap;
-        return TRT_OK;
-    }
-    const size_t ev_s = b.ev_chunks / trt::kDeferStripes, q_s = b.shq_cap / trt::kDeferStripes;
-    for (uint32_t s = 0; s < trt::kDeferStripes; ++s) { // taken = min(requested, stripe capacity)
+    // taken = min(requested, the stripe capacity the slot's last frame ran with: its own size or
+    // a test hook's, not the slot's allocation, which may be larger)
+    const size_t ev_s = b.used_ev_cap, q_s = b.used_shq_cap;
+    for (uint32_t s = 0; s < trt::kDeferStripes; ++s) {
         out[0] += std::min<size_t>(d.chunks[s * trt::kCtrStride], ev_s);
         out[1] += std::min<size_t>(d.nq[s * trt::kCtrStride], q_s);
     }
@@ -529,20 +498,9 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
         if (trt::collapse_bvh4(bvh, bvh4) > (uint32_t)trt::kBvhStack) bvh4.clear();
         bvh4_n = bvh4.size();
         std::vector<trt::Bvh4QNode> bvh4q;
-        std::vector<trt::Bvh4CNode> bvh4c;
         const bool quant = !bvh4.empty() && trt::quantize_bvh4(bvh4, bvh4q);
-        // the 48-B form of the quantized nodes reorders the leaf triangles (and remaps the leaf
-        // references of every walk), so it is made before anything is uploaded
-        if (quant && bvh_compress_mode() != 0) {
-            if (!trt::compress_bvh4(bvh, bvh4, bvh4q, bvh_tris, bvh4c)) bvh4c.clear();
-        }
         if (quant && (rc = upload((void**)&c->d_bvh4q, bvh4q.data(), sizeof(trt::Bvh4QNode) * bvh4q.size(),
                                   "upload quantized bvh4")) != TRT_OK) {
-            free_scene(c);
-            return rc;
-        }
-        if (!bvh4c.empty() && (rc = upload((void**)&c->d_bvh4c, bvh4c.data(), sizeof(trt::Bvh4CNode) * bvh4c.size(),
-                                           "upload compressed bvh4")) != TRT_OK) {
             free_scene(c);
             return rc;
         }
@@ -576,7 +534,6 @@ int trt_upload_scene(trt_ctx* c, const trt_ubo* ubo, const trt_triangle* tris, u
     }
     if (c->d_bvh4) sb[trt::kSceneBvh4] = sizeof(trt::Bvh4Node) * bvh4_n;
     if (c->d_bvh4q) sb[trt::kSceneBvh4Q] = sizeof(trt::Bvh4QNode) * bvh4_n;
-    if (c->d_bvh4c) sb[trt::kSceneBvh4C] = sizeof(trt::Bvh4CNode) * bvh4_n;
     if (c->d_env) sb[trt::kSceneEnv] = (size_t)env_w * env_h * 4;
     c->nbatch = nmodel;
     c->top = top;
@@ -682,7 +639,6 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // GEOM 3 kernels walk only the quantized nodes (trt_kernel.hip g3_quant_only): a scene whose
     // nodes did not quantize (or whose 4-wide stack would not fit) takes the GEOM 2 kernels.
     A.bvh_waves4 = c->d_bvh4q ? (c->bvh_waves4 >= 0 ? (uint32_t)c->bvh_waves4 : 1u) : 0u;
-    A.bvh4q_n = c->d_bvh4q ? (uint32_t)(c->scene_bytes[trt::kSceneBvh4Q] / sizeof(trt::Bvh4QNode)) : 0u;
     A.xcd_rot = c->xcd_rot;
     A.xcd_skew = c->xcd_skew;
     A.xcd_inter = c->xcd_inter;
@@ -702,8 +658,6 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // profiles/r03_ab_frame_pair.log
     A.frame_group = c->frame_group > 0 ? (uint32_t)c->frame_group : (c->nbatch == 0 ? 2u : 1u);
     // 48-B nodes (TRT_BVH_COMPRESS, opt-in; 0 = off is the default): for the 4-wave build (mode 1) or for every BVH4 walk (mode 2)
-    const int cm = bvh_compress_mode();
-    A.bvh4c = (c->d_bvh4c && (cm == 2 || (cm == 1 && A.bvh_waves4))) ? c->d_bvh4c : nullptr;
 }
 
 // Does this frame run deferred shadows?  Auto: mesh scenes with max_depth >= 8, whose deep
@@ -747,7 +701,7 @@ size_t env_cap(const char* name, size_t v) {
 
 // ---- deferred-frame scratch (one set per frames-in-flight slot) ----------------------------
 
-// Pool-design sizes (and the pass-B query queue of TRT_DEFER_LEVELS_B): event chunks (per tile:
+// Deferred-frame sizes: event chunks (per tile:
 // ceil((2^D - 1) / kEvRows) at depth <= 4, else 4 on average, at least 128 per stripe) and
 // shadow queries (6 per pixel on average), both split into kDeferStripes equal stripes (tile t
 // uses stripe hash(t)); ~1.2 KB per pixel at depth >= 5 (16 events of 64 B + 6 queries of 32 B).
@@ -769,44 +723,21 @@ size_t shadow_qcap(size_t ntiles) {
     const size_t tiles_per_stripe = (ntiles + S - 1) / S;
     return S * std::min<size_t>(std::max<size_t>(6 * tiles_per_stripe * 64u, 1u << 12), 0xFFFFFFFFu / S);
 }
-// Level designs: kLvEvPerPixel event slots per pixel on average (the shipped frame logs 1.9) and
-// one queue entry per pixel per level (a level with more children than the frame has pixels
-// hands the rest to the fallback).
-constexpr size_t kLvEvPerPixel = 4;
-
 struct DeferSizes {
-    size_t chunks = 0, qcap = 0;           // pool-format events (chunks) and shadow queries
-    size_t lv_evcap = 0, lv_qcap = 0;      // TRT_DEFER_LEVELS events / either level design's queues
-    bool links = false;                    // TRT_DEFER_LEVELS_B: queue entries carry parent links
+    size_t chunks = 0, qcap = 0; // event chunks and shadow queries
     size_t bytes = 0;
 };
-DeferSizes defer_sizes(int design, size_t ntiles, uint32_t D, size_t npx) {
+DeferSizes defer_sizes(size_t ntiles, uint32_t D, size_t npx) {
     DeferSizes z;
-    if (design == TRT_DEFER_POOL) {
-        z.chunks = pool_chunks(ntiles, D);
-        z.qcap = shadow_qcap(ntiles);
-    } else {
-        z.lv_qcap = std::min<size_t>(npx, 0x7FFFFFFFu);
-        if (design == TRT_DEFER_LEVELS) {
-            z.lv_evcap = std::min<size_t>(npx * kLvEvPerPixel, 0xFFFFFFF0u);
-        } else {
-            constexpr size_t S = trt::kDeferStripes, slots = trt::kEvRows * 64u;
-            const size_t want = std::min<size_t>(npx * kLvEvPerPixel, (1u << 30) - 1u);
-            z.chunks = ((want + slots - 1) / slots + S - 1) / S * S;
-            z.qcap = shadow_qcap(ntiles);
-            z.links = true;
-        }
-    }
-    z.bytes = z.chunks * kPoolEvBytes + z.qcap * 2 * sizeof(float4) +
-              z.lv_evcap * (sizeof(float4) + sizeof(uint32_t)) +
-              2 * z.lv_qcap * (2 * sizeof(float4) + (z.links ? sizeof(uint32_t) : 0)) +
-              npx * (sizeof(uint2) + 2 * sizeof(uint32_t)) + sizeof(trt::LevCtr) + sizeof(trt::DeferCtr);
+    z.chunks = pool_chunks(ntiles, D);
+    z.qcap = shadow_qcap(ntiles);
+    z.bytes = z.chunks * kPoolEvBytes + z.qcap * 2 * sizeof(float4) + npx * (sizeof(uint2) + sizeof(uint32_t)) +
+              sizeof(trt::DeferCtr);
     return z;
 }
 
 bool defer_bufs_fit(const trt_ctx::SplitBufs& b, const DeferSizes& z, size_t npx) {
-    return z.chunks <= b.ev_chunks && z.qcap <= b.shq_cap && z.lv_evcap <= b.lv_evcap && z.lv_qcap <= b.lv_qcap &&
-           (!z.links || b.lv_qlink[0]) && npx <= b.dnpx;
+    return z.chunks <= b.ev_chunks && z.qcap <= b.shq_cap && npx <= b.dnpx;
 }
 
 // Device bytes one frames-in-flight slot needs for a deferred frame of these params (0 when
@@ -814,13 +745,12 @@ bool defer_bufs_fit(const trt_ctx::SplitBufs& b, const DeferSizes& z, size_t npx
 size_t defer_slot_bytes(const trt_ctx* c, const trt_params* p, uint32_t slot) {
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     const size_t ntiles = ((p->width + 7u) / 8u) * ((trt_output_rows(p) + 7u) / 8u);
-    const DeferSizes z = defer_sizes(c->defer_design, ntiles, p->max_depth, npx);
+    const DeferSizes z = defer_sizes(ntiles, p->max_depth, npx);
     return defer_bufs_fit(c->split[slot], z, npx) ? 0 : z.bytes;
 }
 
 // The automatic frames-in-flight count of a deferred loop, bounded by device memory: each slot
-// holds its own scratch (defer_sizes: the shipped 1024x768 frame ~1 GB per slot in the pool
-// design, ~120 MB in TRT_DEFER_LEVELS), and the slots that would still need allocating may take
+// holds its own scratch (defer_sizes: the shipped 1024x768 frame ~1 GB per slot), and the slots that would still need allocating may take
 // at most half of the free device memory.
 uint32_t fit_defer_slots(const trt_ctx* c, const trt_params* p, uint32_t want) {
     size_t freeb = 0, total = 0;
@@ -835,60 +765,41 @@ uint32_t fit_defer_slots(const trt_ctx* c, const trt_params* p, uint32_t want) {
 }
 
 void free_defer_bufs(trt_ctx::SplitBufs& b) {
-    void* ps[] = {b.ev, b.shq, b.px_ev, b.fb, b.lv_ev, b.lv_evr, b.lv_q[0], b.lv_q[1], b.lv_qlink[0], b.lv_qlink[1],
-                  b.lv_flag};
+    void* ps[] = {b.ev, b.shq, b.px_ev, b.fb};
     for (void* q : ps) (void)hipFree(q);
     b.ev = nullptr;
     b.shq = nullptr;
     b.px_ev = nullptr;
     b.fb = nullptr;
-    b.lv_ev = nullptr;
-    b.lv_evr = nullptr;
-    b.lv_q[0] = b.lv_q[1] = nullptr;
-    b.lv_qlink[0] = b.lv_qlink[1] = nullptr;
-    b.lv_flag = nullptr;
     b.ev_chunks = b.shq_cap = b.dnpx = 0;
-    b.lv_evcap = b.lv_qcap = b.lv_npx = 0;
 }
 
-// Allocates slot `slot`'s deferred-frame scratch (the context's design) for this frame and fills
+// Allocates slot `slot`'s deferred-frame scratch for this frame and fills
 // A's defer fields.
 int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     auto& b = c->split[slot];
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
-    const int design = c->defer_design;
-    const DeferSizes z = defer_sizes(design, A.ntiles, p->max_depth, npx);
+    const DeferSizes z = defer_sizes(A.ntiles, p->max_depth, npx);
     if (!defer_bufs_fit(b, z, npx)) {
         free_defer_bufs(b);
         hipError_t e = hipSuccess;
         auto alloc = [&](void** q, size_t bytes) {
             if (e == hipSuccess && bytes) e = hipMalloc(q, bytes);
         };
+        if ((int)slot == test_fail_defer_slot()) e = hipErrorOutOfMemory;
         alloc((void**)&b.ev, z.chunks * kPoolEvBytes);
         alloc((void**)&b.shq, z.qcap * 2 * sizeof(float4));
-        alloc((void**)&b.lv_ev, z.lv_evcap * sizeof(float4));
-        alloc((void**)&b.lv_evr, z.lv_evcap * sizeof(uint32_t));
-        for (int k = 0; k < 2; ++k) {
-            alloc((void**)&b.lv_q[k], z.lv_qcap * 2 * sizeof(float4));
-            if (z.links) alloc((void**)&b.lv_qlink[k], z.lv_qcap * sizeof(uint32_t));
-        }
         alloc((void**)&b.px_ev, npx * sizeof(uint2));
-        alloc((void**)&b.lv_flag, npx * sizeof(uint32_t));
         alloc((void**)&b.fb, npx * sizeof(uint32_t));
         if (!b.dctr) alloc((void**)&b.dctr, sizeof(trt::DeferCtr));
-        if (!b.lv_ctr) alloc((void**)&b.lv_ctr, sizeof(trt::LevCtr));
         if (e != hipSuccess) {
             free_defer_bufs(b);
             return hip_fail(c, e, "alloc deferred-frame buffers");
         }
         b.ev_chunks = z.chunks;
         b.shq_cap = z.qcap;
-        b.lv_evcap = z.lv_evcap;
-        b.lv_qcap = z.lv_qcap;
-        b.dnpx = b.lv_npx = npx;
+        b.dnpx = npx;
     }
-    b.last_levels = design == TRT_DEFER_LEVELS;
-    b.last_npx = npx;
     A.defer = 1;
     // pass-A waves per tile (pool design): explicit (TRT_DEFER_PPW), else by the frames that
     // overlap: with few frames in flight a frame's latency — its deepest tile's chain of
@@ -896,8 +807,6 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
     // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
     A.defer_sub = c->defer_sub ? c->defer_sub : (c->cur_in_flight <= 4u ? 2u : 1u);
-    A.lv = design == TRT_DEFER_LEVELS ? 1u : design == TRT_DEFER_LEVELS_B ? 2u : 0u;
-    A.lv_level = 0;
     // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
     A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", z.chunks / trt::kDeferStripes);
     A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", z.qcap / trt::kDeferStripes);
@@ -906,17 +815,8 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     A.px_ev = b.px_ev;
     A.fb = b.fb;
     A.dctr = b.dctr;
-    const size_t lv_slots = design == TRT_DEFER_LEVELS ? z.lv_evcap : z.chunks * trt::kEvRows * 64u;
-    A.lv_evcap = (uint32_t)std::max<size_t>(env_cap("TRT_LV_EVCAP", lv_slots), npx);
-    A.lv_qcap = (uint32_t)env_cap("TRT_LV_QCAP", z.lv_qcap);
-    A.lv_ev = b.lv_ev;
-    A.lv_evr = b.lv_evr;
-    A.lv_q[0] = b.lv_q[0];
-    A.lv_q[1] = b.lv_q[1];
-    A.lv_qlink[0] = b.lv_qlink[0];
-    A.lv_qlink[1] = b.lv_qlink[1];
-    A.lv_ctr = b.lv_ctr;
-    A.lv_flag = b.lv_flag;
+    b.used_ev_cap = A.ev_cap;
+    b.used_shq_cap = A.shq_cap;
     return TRT_OK;
 }
 
@@ -927,14 +827,12 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     A.split_w = 0;
     A.split_d1 = A.max_depth;
     A.num_cus = c->num_cus;
-    A.persist = c->d_persist + (size_t)slot * kPersistWords;
     A.defer = 0;
-    A.lv = 0;
     const bool defer = defer_frame(c, p);
     // A COUNT frame of a scene whose frames run deferred is traced unsplit, so its image is the
     // deferred frame's bit for bit (both are the reference's single running sum; a deferred
     // frame's subtree split keeps that order through LINK events).
-    if ((defer && c->defer_design == TRT_DEFER_POOL) || !defer_frame(c, p, true)) A.split_w = split_window(c, p);
+    if (defer || !defer_frame(c, p, true)) A.split_w = split_window(c, p);
     if (!A.split_w && !defer) return TRT_OK;
     auto& b = c->split[slot];
     if (b.last && b.last != stream) HIP_TRY(c, hipStreamWaitEvent(stream, b.done, 0));
@@ -984,56 +882,6 @@ int prepare_split(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot, hipS
     A.acc = b.acc;
     A.spilled = b.spilled;
     A.ctr = b.ctr;
-    return TRT_OK;
-}
-
-// Hot-first dealing (trt_kernel.hip trace_hot) for a single-frame plain launch on `slot`: the
-// slot's lists (allocated, or cleared when the tiling changed) and the rotation step.  The
-// lists belong to the stream of the slot's first such frame; a frame on another stream deals
-// plainly and leaves them alone, so every read and write of them is ordered by that one stream
-// (no cross-stream waits).  Other launches get hot_max = 0.
-int prepare_hot(trt_ctx* c, KArgs& A, uint32_t slot, hipStream_t stream, bool count) {
-    A.hot = nullptr;
-    A.hot_flag = nullptr;
-    A.hot_max = A.hot_k = A.hot_fstride = 0;
-    if (!c->hot_first || count || A.split_w || A.defer || A.nframes > 1u || A.spp_lanes || A.ntiles < 64u) return TRT_OK;
-    auto& b = c->split[slot];
-    if (b.hot && b.hot_stream != stream) return TRT_OK;
-    static const uint32_t cap = [] {
-        const char* e = std::getenv("TRT_HOT_MAX");
-        return e ? std::max<uint32_t>(1u, (uint32_t)std::strtoul(e, nullptr, 10)) : 512u;
-    }();
-    const uint32_t hmax = std::max<uint32_t>(1u, std::min<uint32_t>(cap, A.ntiles / 16u));
-    if (!b.hot || A.ntiles > b.hot_cap || hmax != b.hot_max) {
-        if (b.hot) HIP_TRY(c, hipStreamSynchronize(b.hot_stream)); // its frames read the old lists
-        (void)hipFree(b.hot);
-        (void)hipFree(b.hot_flag);
-        b.hot = nullptr;
-        b.hot_flag = nullptr;
-        b.hot_cap = b.hot_tiles = 0;
-        hipError_t e = hipMalloc((void**)&b.hot, 3 * (size_t)(hmax + 2u) * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMalloc((void**)&b.hot_flag, 3 * (size_t)A.ntiles);
-        if (e != hipSuccess) {
-            (void)hipFree(b.hot);
-            b.hot = nullptr;
-            return hip_fail(c, e, "alloc hot-first lists");
-        }
-        b.hot_cap = A.ntiles;
-        b.hot_max = hmax;
-        b.hot_stream = stream;
-    }
-    if (b.hot_tiles != A.ntiles) { // another tiling: the lists index other tiles
-        HIP_TRY(c, hipMemsetAsync(b.hot, 0, 3 * (size_t)(b.hot_max + 2u) * sizeof(uint32_t), stream));
-        HIP_TRY(c, hipMemsetAsync(b.hot_flag, 0, 3 * (size_t)b.hot_cap, stream));
-        b.hot_tiles = A.ntiles;
-        b.hot_k = 0;
-    }
-    A.hot = b.hot;
-    A.hot_flag = b.hot_flag;
-    A.hot_max = b.hot_max;
-    A.hot_fstride = b.hot_cap;
-    A.hot_k = b.hot_k;
-    b.hot_k = (b.hot_k + 1u) % 3u;
     return TRT_OK;
 }
 
@@ -1089,7 +937,7 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     // Plain frames (no subtree split, no deferred shadows: the same decision prepare_split
     // makes) go out several per launch; the others one per launch (per-slot scratch).
     const bool defer = defer_frame(c, p);
-    const bool split = ((defer && c->defer_design == TRT_DEFER_POOL) || !defer_frame(c, p, true)) && split_window(c, p) != 0;
+    const bool split = (defer || !defer_frame(c, p, true)) && split_window(c, p) != 0;
     const bool plain = !defer && !split;
     // Frames in flight (main.cpp:45, MAX_FRAMES_IN_FLIGHT): launch j runs on slot j % n.  Slot 0
     // is the context's stream, slots 1..n-1 are context-owned streams forked from it here and
@@ -1153,9 +1001,11 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
         for (uint32_t k = 0; k < n; ++k) fill_frame(A.fr[k], ubo_of(i0 + k), frames[i0 + k].out8, frames[i0 + k].in_place);
         uint32_t slot = j % nfl;
         if ((rc = prepare_split(c, p, A, slot, sv[slot])) != TRT_OK) {
-            // auto count: a slot whose scratch cannot be allocated is dropped, with the slots
-            // after it; the launch goes to a slot that has its scratch
-            if (c->frames_in_flight || slot == 0) return rc;
+            // auto count: a slot whose scratch does not fit in device memory is dropped, with the
+            // slots after it, and the launch goes to a slot that has its scratch; any other
+            // failure is the caller's
+            if (c->frames_in_flight || slot == 0 || rc != TRT_ERR_OOM) return rc;
+            (void)hipGetLastError(); // the failed hipMalloc's sticky error: not the next launch's
             c->err.clear();
             nfl = slot;
             c->cur_in_flight = nfl;
@@ -1163,7 +1013,6 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
             if ((rc = prepare_split(c, p, A, slot, sv[slot])) != TRT_OK) return rc;
         }
         hipStream_t st = sv[slot];
-        if ((rc = prepare_hot(c, A, slot, st, false)) != TRT_OK) return rc;
         const bool timed = timing && j % every == 0;
         const size_t k = 2 * (size_t)(j / every);
         if (timed) HIP_TRY(c, hipEventRecord(c->fev[k], st));
@@ -1270,7 +1119,6 @@ int trt_render(trt_ctx* c, const trt_params* p, uint8_t* out8, float* out32, trt
     const uint32_t slot = render_slot(c, c->stream);
     c->cur_in_flight = 1u; // one frame: its latency is the rate
     if ((rc = prepare_split(c, p, A, slot, c->stream)) != TRT_OK) return rc;
-    if ((rc = prepare_hot(c, A, slot, c->stream, count)) != TRT_OK) return rc;
     if (count) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 32 * sizeof(unsigned long long), c->stream));
     if (timing) HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     if (npx > 0) HIP_TRY(c, trt::launch_trace(A, c->stream, count));
@@ -1392,7 +1240,6 @@ void** scene_buf(trt_ctx* c, int k) {
     case kSceneShade: return reinterpret_cast<void**>(&c->d_shade);
     case kSceneMats: return reinterpret_cast<void**>(&c->d_mats);
     case kSceneBvh4Q: return reinterpret_cast<void**>(&c->d_bvh4q);
-    case kSceneBvh4C: return reinterpret_cast<void**>(&c->d_bvh4c);
     default: return reinterpret_cast<void**>(&c->d_env);
     }
 }
@@ -1452,22 +1299,6 @@ extern "C" int trt_diag_defer_pad(trt_ctx* c, uint32_t slot, uint32_t* out16) {
     return TRT_OK;
 }
 
-// diagnostic: slot `slot`'s hot-first lists (trt_kernel.hip trace_hot): out[0..5] = (count,
-// longest wave in 10-ns ticks) of lists 0..2, out[6] = the list the slot's next frame reads,
-// out[7] = hot_max (0: the slot has run no hot-first frame).
-extern "C" int trt_diag_hot(trt_ctx* c, uint32_t slot, uint32_t* out8) {
-    if (!c || !out8 || slot >= TRT_BUILD_MAX_IN_FLIGHT) return TRT_ERR_INVALID;
-    const auto& b = c->split[slot];
-    std::memset(out8, 0, 8 * sizeof(uint32_t));
-    if (!b.hot) return TRT_OK;
-    HIP_TRY(c, hipDeviceSynchronize());
-    for (uint32_t l = 0; l < 3; ++l)
-        HIP_TRY(c, hipMemcpy(out8 + 2 * l, b.hot + (size_t)l * (b.hot_max + 2u), 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    out8[6] = b.hot_k;
-    out8[7] = b.hot_max;
-    return TRT_OK;
-}
-
 extern "C" int trt_diag_set_buffer(trt_ctx* c, void* dev_ptr) {
     if (!c) return TRT_ERR_INVALID;
     c->diag = dev_ptr;
@@ -1496,11 +1327,6 @@ extern "C" int trt_diag_shadow_batch(trt_ctx* c, const trt_params* p, const void
     return TRT_OK;
 }
 
-// Host-only check of the BVH pipeline of trt_upload_scene (no GPU): BVH2 build, 4-wide
-// collapse, quantization and the 48-B compression with its self-check.  out[0] BVH2 nodes,
-// out[1] BVH4 nodes, out[2] quantized (0/1), out[3] compressed (0/1), out[4] worst-case BVH4
-// stack, out[5] leaf triangles.  Returns TRT_ERR_INVALID when no BVH is built (overlapping
-// batch ranges).
 // Diagnostic (tests/test_bvh_layout.py): the BVH2 the upload builds — nodes and the BVH-ordered
 // leaf triangle records (meta: triangle, batch, ni) — copied out when the capacities suffice;
 // counts[0] = nodes, counts[1] = leaf references.
@@ -1518,6 +1344,10 @@ extern "C" int trt_diag_bvh_export(const trt_triangle* tris, uint32_t ntri, cons
     return TRT_OK;
 }
 
+// Host-only check of the BVH pipeline of trt_upload_scene (no GPU): BVH2 build, 4-wide
+// collapse and quantization.  out[0] BVH2 nodes, out[1] BVH4 nodes, out[2] quantized (0/1),
+// out[3] BVH2 depth (levels of the deepest leaf, root = 1), out[4] worst-case BVH4 stack,
+// out[5] leaf triangles.  Returns TRT_ERR_INVALID when no BVH is built (overlapping batch ranges).
 extern "C" int trt_diag_bvh_build(const trt_triangle* tris, uint32_t ntri, const trt_model* models, uint32_t nmodel,
                                   uint64_t out[6]) {
     if (!out || (ntri && !tris) || (nmodel && !models)) return TRT_ERR_INVALID;
@@ -1530,9 +1360,8 @@ extern "C" int trt_diag_bvh_build(const trt_triangle* tris, uint32_t ntri, const
     out[4] = trt::collapse_bvh4(bvh, bvh4);
     out[1] = bvh4.size();
     std::vector<trt::Bvh4QNode> q;
-    std::vector<trt::Bvh4CNode> cn;
     out[2] = (!bvh4.empty() && trt::quantize_bvh4(bvh4, q)) ? 1 : 0;
-    out[3] = (out[2] && trt::compress_bvh4(bvh, bvh4, q, bvh_tris, cn)) ? 1 : 0;
+    out[3] = trt::bvh_depth(bvh);
     out[5] = bvh_tris.size();
     return TRT_OK;
 }

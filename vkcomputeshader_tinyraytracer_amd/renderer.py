@@ -77,16 +77,10 @@ class Renderer:
         2 = on."""
         self._check(self._L.trt_set_deferred_shadows(self._h, int(mode)))
 
-    def set_defer_design(self, design: int) -> None:
-        """trt_set_defer_design: 0 = pool (default: per-tile segment pool + a dense shadow pass),
-        1 = levels (breadth first, one launch per depth, inline shadow rays), 2 = levels_b (the
-        levels with the dense shadow pass)."""
-        self._check(self._L.trt_set_defer_design(self._h, int(design)))
-
     def defer_stats(self, slot: int = 0) -> dict:
-        """trt_defer_stats of in-flight slot `slot` (waits for the context's stream).  Pool design:
-        event chunks / shadow queries and their capacities; level design: events written / the
-        largest level queue and their capacities (same keys)."""
+        """trt_defer_stats of in-flight slot `slot` (waits for the context's stream): event
+        chunks taken / shadow queries appended, pixels re-traced in place, and the slot's
+        capacities."""
         out = (ctypes.c_uint64 * 5)()
         self._check(self._L.trt_defer_stats(self._h, int(slot), out))
         return {"chunks": out[0], "queries": out[1], "fallback_pixels": out[2], "chunk_cap": out[3],
