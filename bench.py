@@ -724,17 +724,18 @@ def c_abi_leg(frames: int) -> dict:
     once with 32 queues (what the Python package and this bench export)."""
     out = {"note": "tests/native/drop_in_host --bench: trt_render_frames of the camera walk (auto in-flight "
                    "count) and trt_render per frame into host memory (drawFrame pacing)"}
-    for key, queues in (("default_env", None), ("queues_32", "32")):
+    for key, queues, inflight in (("default_env", None, 0), ("queues_32", "32", 0)):
         env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "LD_LIBRARY_PATH")}
         if queues:
             env["GPU_MAX_HW_QUEUES"] = queues
-        r = subprocess.run([str(DROPIN_HOST), "--bench", str(DROPIN_DUMP), str(frames)], capture_output=True,
-                           text=True, timeout=600, env=env)
+        r = subprocess.run([str(DROPIN_HOST), "--bench", str(DROPIN_DUMP), str(frames), str(inflight)],
+                           capture_output=True, text=True, timeout=600, env=env)
         if r.returncode != 0:
             out[key] = {"error": r.stderr[-500:]}
             continue
         line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and "bench" in x][-1]
-        out[key] = {k: line[k] for k in ("gpu_max_hw_queues", "ms_per_frame", "fps", "draw_frame_ms", "frames")}
+        out[key] = {k: line[k] for k in ("gpu_max_hw_queues", "in_flight_setting", "ms_per_frame", "fps",
+                                         "draw_frame_ms", "frames")}
     return out
 
 

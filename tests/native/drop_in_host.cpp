@@ -238,21 +238,17 @@ int bench(const std::vector<Mesh>& meshes, uint32_t frames, uint32_t in_flight) 
     trt_params rp;
     trt_params_default(&rp); // 1024x768, depth 20, reference flags
     const size_t fb = (size_t)rp.width * rp.height * 4;
-    const uint32_t nbuf = 16; // distinct images for concurrent frames
-    uint8_t* dev = nullptr;
-    hcheck(hipMalloc(reinterpret_cast<void**>(&dev), nbuf * fb), "hipMalloc");
+    uint8_t* dev = nullptr; // one image per frame: the frames of the loop run concurrently
+    hcheck(hipMalloc(reinterpret_cast<void**>(&dev), (size_t)frames * fb), "hipMalloc");
     trt_params p = rp;
     p.flags |= TRT_FLAG_DEVICE_PTRS;
     const std::vector<trt_ubo> walk = camera_walk(frames);
     using clk = std::chrono::steady_clock;
-    auto run_loop = [&](uint32_t n) { // n frames of the walk, frame i into image i % nbuf
-        for (uint32_t i0 = 0; i0 < n; i0 += nbuf) {
-            const uint32_t k = std::min(nbuf, n - i0);
-            check(trt_render_frames(ctx, &p, walk.data() + i0, k, dev, fb, 0), "trt_render_frames", ctx);
-        }
+    auto run_loop = [&](uint32_t n) { // the first n frames of the walk in one frame-loop call
+        check(trt_render_frames(ctx, &p, walk.data(), n, dev, fb, 0), "trt_render_frames", ctx);
         check(trt_synchronize(ctx), "trt_synchronize", ctx);
     };
-    run_loop(std::min(frames, 2 * nbuf)); // warmup: scratch, streams, clocks
+    run_loop(std::min(frames, 32u)); // warmup: scratch, streams, clocks
     const auto t0 = clk::now();
     run_loop(frames);
     const double loop_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();

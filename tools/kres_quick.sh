@@ -9,4 +9,4 @@ FP="-ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-de
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP "-DTRT_KRES_ONLY=$K" "$@" --cuda-device-only -c \
     -o /tmp/kres_quick.co "$ROOT/vkcomputeshader_tinyraytracer_amd/csrc/trt_kernel.hip" -Rpass-analysis=kernel-resource-usage 2>&1 \
     | sed 's/.*remark: //; s/ \[-Rpass-analysis=kernel-resource-usage\]//' \
-    | awk '/^Function Name:/ {show = ($0 ~ /trace_|defer_/)} show && /Function Name|VGPRs|Spill|ScratchSize|Occupancy|LDS Size/ {print}'
+    | awk '/^Function Name:/ {show = ($0 ~ /trace_|defer_|share_/)} show && /Function Name|VGPRs|Spill|ScratchSize|Occupancy|LDS Size/ {print}'

@@ -46,6 +46,28 @@ for stage in "$@"; do
       step "kb_${cfg}" 300 python tools/kbench.py --config "$cfg" $args --tag "$leg"
       grep '^{' "$OUT/kb_${cfg}.log" >> "$OUT/kb.jsonl"
     done ;;
+  pytest) # the test files named in TESTS
+    step "pytest_${TESTS_TAG:-sel}" 900 $PYT $TESTS ;;
+  share_ab) # subtree hand-off of single-frame C2 launches: on / off, interleaved rounds
+    for round in 1 2; do
+      for sh in 1 0; do
+        for cf in "--frame-batch 1 --inflight 1" "--frame-batch 1 --inflight 2" "--frame-batch 20"; do
+          TRT_SHARE=$sh timeout -k 10 200 python tools/kbench.py --config C2 --frames 300 $cf --tag "share$sh:$cf" \
+            >> "$OUT/share_ab.jsonl" 2>> "$OUT/share_ab.err" || { tail -5 "$OUT/share_ab.err"; exit 1; }
+        done
+      done
+    done
+    python tools/ab_summary.py "$OUT/share_ab.jsonl" ;;
+  cabi) # the shipped frame through the C++ host: HIP's default queues (auto / 4 in flight), 32 queues
+    for cf in "unset 0" "unset 4" "unset 2" "32 0"; do
+      set -- $cf
+      if [ "$1" = unset ]; then
+        env -u GPU_MAX_HW_QUEUES timeout -k 10 200 tests/native/drop_in_host --bench tests/golden/dropin_meshes.bin 160 "$2" >> "$OUT/cabi.log" 2>&1 || exit 1
+      else
+        GPU_MAX_HW_QUEUES=$1 timeout -k 10 200 tests/native/drop_in_host --bench tests/golden/dropin_meshes.bin 160 "$2" >> "$OUT/cabi.log" 2>&1 || exit 1
+      fi
+    done
+    grep bench "$OUT/cabi.log" ;;
   *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

@@ -33,10 +33,10 @@ def main():
     with open(out, "w", newline="") as f:
         w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
         w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev",
-                    "Workgroups"])
+                    "Workgroups", "MedianNs"])
         for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
             w.writerow([name, len(v), int(sum(v)), sum(v) / len(v), round(100.0 * sum(v) / total, 2), int(min(v)),
-                        int(max(v)), statistics.pstdev(v) if len(v) > 1 else 0.0, wg[name]])
+                        int(max(v)), statistics.pstdev(v) if len(v) > 1 else 0.0, wg[name], statistics.median(v)])
 
 
 if __name__ == "__main__":

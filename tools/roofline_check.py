@@ -24,17 +24,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--csv", required=True)
     ap.add_argument("--kernel", required=True, help="regex over kernel names (summed)")
-    ap.add_argument("--frames", type=int, required=True, help="frames traced by the matching launches")
+    ap.add_argument("--frames", type=int, default=0, help="frames traced by the matching launches (total time / frames)")
+    ap.add_argument("--frames-per-call", type=int, default=0,
+                    help="instead: frames each matching launch traces; kernel time = the median launch / this "
+                         "(the CSV's MedianNs, tools/rocpd_stats.py)")
     ap.add_argument("--bench", required=True, help="log holding the bench JSON line")
     ap.add_argument("--key", default="roofline", help="dotted path of the roofline object in the line")
     a = ap.parse_args()
     rx = re.compile(a.kernel)
-    total_ns, calls = 0.0, 0
+    total_ns, calls, median_ns = 0.0, 0, None
     with open(a.csv) as f:
         for row in csv.DictReader(f):
             if rx.search(row["Name"]):
                 total_ns += float(row["TotalDurationNs"])
                 calls += int(row["Calls"])
+                median_ns = float(row["MedianNs"]) if row.get("MedianNs") else None
     line = None
     for s in open(a.bench):
         if s.startswith("{"):
@@ -42,7 +46,11 @@ def main():
     rl = line
     for k in a.key.split("."):
         rl = rl[k]
-    us = total_ns / a.frames / 1e3
+    if a.frames_per_call:
+        assert median_ns is not None, "the CSV has no MedianNs column (tools/rocpd_stats.py)"
+        us = median_ns / a.frames_per_call / 1e3
+    else:
+        us = total_ns / a.frames / 1e3
     frac = rl["flops_per_frame"] / (us * 1e-6) / 1e12 / PEAK_TF
     out = {"calls": calls, "frames": a.frames, "kernel_us_per_frame_csv": round(us, 3),
            "kernel_frac_csv": round(frac, 4), "kernel_us_per_frame_line": rl.get("kernel_us_per_frame"),
