@@ -53,6 +53,7 @@ for v in "$@"; do
         notrig) variant notrig -DTRT_DIAG_NO_UV_TRIG ;;
         clock) variant clock -DTRT_DIAG_WAVE_CLOCK ;;
         work) variant work -DTRT_DIAG_PIXEL_WORK ;;
+        passa) variant passa -DTRT_DIAG_PASSA_STEPS ;;
         prev) # the kernel of git revision $PREV (default HEAD), for A/B against the work tree
             git -C "$ROOT" show "${PREV:-HEAD}:vkcomputeshader_tinyraytracer_amd/csrc/trt_kernel.hip" > "$SRC/.prev_kernel.hip"
             KSRC="$SRC/.prev_kernel.hip" variant prev

@@ -48,16 +48,20 @@ for stage in "$@"; do
     done ;;
   pytest) # the test files named in TESTS
     step "pytest_${TESTS_TAG:-sel}" 900 $PYT $TESTS ;;
-  share_ab) # subtree hand-off of single-frame C2 launches: on / off, interleaved rounds
-    for round in 1 2; do
-      for sh in 1 0; do
-        for cf in "--frame-batch 1 --inflight 1" "--frame-batch 1 --inflight 2" "--frame-batch 20"; do
-          TRT_SHARE=$sh timeout -k 10 200 python tools/kbench.py --config C2 --frames 300 $cf --tag "share$sh:$cf" \
-            >> "$OUT/share_ab.jsonl" 2>> "$OUT/share_ab.err" || { tail -5 "$OUT/share_ab.err"; exit 1; }
+  ab) # interleaved A/B of library builds: AB_LIBS="name:path ..." (empty path = the product),
+      # AB_LEGS="config|args;config|args" (kbench), AB_ROUNDS rounds
+    IFS=';' read -ra legs <<< "${AB_LEGS:-C2|--frames 200 --frame-batch 20}"
+    for round in $(seq 1 "${AB_ROUNDS:-2}"); do
+      for lib in ${AB_LIBS:-cur:}; do
+        name=${lib%%:*}; path=${lib#*:}
+        for leg in "${legs[@]}"; do
+          cfg=${leg%%|*}; args=${leg#*|}
+          TRT_LIB=$path timeout -k 10 300 python tools/kbench.py --config "$cfg" $args --tag "$name:$cfg:$args" \
+            >> "$OUT/ab.jsonl" 2>> "$OUT/ab.err" || { tail -5 "$OUT/ab.err"; exit 1; }
         done
       done
     done
-    python tools/ab_summary.py "$OUT/share_ab.jsonl" ;;
+    python tools/ab_summary.py "$OUT/ab.jsonl" ;;
   cabi) # the shipped frame through the C++ host: HIP's default queues (auto / 4 in flight), 32 queues
     for cf in "unset 0" "unset 4" "unset 2" "32 0"; do
       set -- $cf

@@ -74,7 +74,6 @@ struct trt_ctx {
     uint32_t defer_sub = 0;
     uint32_t cur_in_flight = 1; // frames in flight of the current render call
     bool spp_lanes = true;      // spp > 1 frames: one lane per sample (TRT_SPP_LANES)
-    bool share = true;          // single-frame triangle-free launches: subtree hand-off (TRT_SHARE)
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.

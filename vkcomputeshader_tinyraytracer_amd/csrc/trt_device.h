@@ -247,7 +247,6 @@ struct KArgs {
     DeferCtr* __restrict__ dctr;
     uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4: trace_tile)
     uint32_t spp_lanes;               // spp > 1: one lane per sample (trace_samples), spp waves per tile
-    uint32_t share;                   // single-frame triangle-free launches: subtree hand-off (share_kernel)
     FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch
 };
 static_assert(sizeof(KArgs) <= 4096, "KArgs fits the 4 KB kernel-argument limit");

@@ -488,14 +488,13 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
                         if (COUNT) ++c.tv;
                 float t = f * dot3(e2, q);
                 if (t <= TRT_EPS) continue;
-                const uint32_t batch = __float_as_uint(g.pad[1]);
+                const uint32_t tri = __float_as_uint(g.pad[0]), batch = __float_as_uint(g.pad[1]);
                 if (SHADOW) {
                     if (!(t < max_dist)) continue;
-                } else if (!(t < best)) { // tie: the smaller (batch, triangle), read back (bvh_leaf)
-                    if (!(t == best && h.kind == HIT_TRI)) continue;
-                    const TriGeo& hb = A.bvh_tris[h.idx];
-                    const uint32_t tri = __float_as_uint(g.pad[0]), bb = __float_as_uint(hb.pad[1]);
-                    if (!(batch < bb || (batch == bb && tri < __float_as_uint(hb.pad[0])))) continue;
+                } else {
+                    const bool better = t < best || (t == best && h.kind == HIT_TRI &&
+                                                     (batch < h.batch || (batch == h.batch && (int)tri < h.idx)));
+                    if (!better) continue;
                 }
                 const BatchRec rec = A.batches[batch]; // the reference's gate for this triangle
                 const bool pass = aabb_hit(o, gate_inv(d), rec.bmin, rec.bmax);
@@ -511,7 +510,11 @@ __device__ __forceinline__ void trace_bvh(const KArgs& A, f3 o, f3 d, f3 inv, Hi
                 best = t;
                 h.t = t;
                 h.kind = HIT_TRI;
-                h.idx = (int)k; // compact hit (bvh_hit_finish)
+                h.idx = (int)tri;
+                h.batch = batch;
+                h.u = u;
+                h.v = v;
+                h.ni = (int)__float_as_uint(g.pad[2]);
             }
         }
         if (stack.sp == 0) return;
@@ -554,16 +557,13 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
                         if (COUNT) ++c.tv;
         float t = f * dot3(e2, q);
         if (t <= TRT_EPS) continue;
-        const uint32_t batch = __float_as_uint(cur.pad[1]);
+        const uint32_t tri = __float_as_uint(cur.pad[0]), batch = __float_as_uint(cur.pad[1]);
         if (SHADOW) {
             if (!(t < max_dist)) continue;
-        } else if (!(t < best)) {
-            // a tie goes to the smaller (batch, triangle): the current best's are read back from
-            // its leaf reference (rare: equal t)
-            if (!(t == best && h.kind == HIT_TRI)) continue;
-            const TriGeo& hb = A.bvh_tris[h.idx];
-            const uint32_t tri = __float_as_uint(cur.pad[0]), bb = __float_as_uint(hb.pad[1]);
-            if (!(batch < bb || (batch == bb && tri < __float_as_uint(hb.pad[0])))) continue;
+        } else {
+            const bool better = t < best || (t == best && h.kind == HIT_TRI &&
+                                             (batch < h.batch || (batch == h.batch && (int)tri < h.idx)));
+            if (!better) continue;
         }
         const BatchRec rec = A.batches[batch]; // the reference's gate for this triangle
         const bool pass = aabb_hit(o, gate_inv(d), rec.bmin, rec.bmax);
@@ -572,33 +572,20 @@ __device__ __forceinline__ bool bvh_leaf(const KArgs& A, uint32_t node, f3 o, f3
             c.bh += pass ? 1u : 0u;
         }
         if (!pass) continue;
-        if (SHADOW) return true;
-        // compact hit: only t and the BVH-ordered reference k are live through the rest of the
-        // walk; bvh_hit_finish recovers the triangle, batch, flag and u, v afterwards
+        if (SHADOW) {
+            h.idx = (int)k; // the occluder's BVH-ordered index (shared with the wave, trace_bvh4)
+            return true;
+        }
         best = t;
         h.t = t;
         h.kind = HIT_TRI;
-        h.idx = (int)k;
+        h.idx = (int)tri;
+        h.batch = batch;
+        h.u = u;
+        h.v = v;
+        h.ni = (int)__float_as_uint(cur.pad[2]);
     }
     return false;
-}
-
-// After a BVH walk whose best hit is a triangle (h.idx = its BVH-ordered reference k): the
-// triangle's index, batch and normal-interpolation flag from the reference record, and u, v by
-// bvh_leaf's own Moller-Trumbore arithmetic on the same operands (bit-identical to the values the
-// walk computed and dropped).
-__device__ __forceinline__ void bvh_hit_finish(const KArgs& A, f3 o, f3 d, Hit& h) {
-    if (h.kind != HIT_TRI) return;
-    const TriGeo g = A.bvh_tris[h.idx];
-    const f3 v0 = ld3(g.v0), e1 = ld3(g.e1), e2 = ld3(g.e2);
-    const f3 hv = cross3(d, e2);
-    const float f = rcp_rn_lane(dot3(e1, hv));
-    const f3 sv = sub(o, v0);
-    h.u = f * dot3(sv, hv);
-    h.v = f * dot3(d, cross3(sv, e1));
-    h.idx = (int)__float_as_uint(g.pad[0]);
-    h.batch = __float_as_uint(g.pad[1]);
-    h.ni = (int)__float_as_uint(g.pad[2]);
 }
 
 // Shadow test of one triangle (BVH-ordered index k, wave-uniform) read through scalar loads:
@@ -1051,7 +1038,6 @@ __device__ __forceinline__ void scene_intersect(const KArgs& A, f3 o, f3 d, Hit&
     if (GEOM >= 2) {
         if (g3_quant_only<GEOM>() || (TRT_BVH_WIDTH == 4 && A.bvh4)) trace_bvh4<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
         else trace_bvh<COUNT, false, GEOM>(A, o, d, inv, h, unused, 0.0f, c, slab);
-        bvh_hit_finish(A, o, d, h);
     }
     else walk_batches<COUNT, false>(A, o, d, inv, h, unused, 0.0f, c, slab);
 }
@@ -2038,11 +2024,44 @@ __device__ __forceinline__ void defer_walk(const KArgs& A, float* lds, float4* s
     PSeg priv[kMaxTreeDepth];
     int pn = 0;
     uint32_t pool_n = 0; // wave-uniform
+#ifdef TRT_DIAG_PASSA_STEPS
+    // diagnostic: per wave, steps and lanes with a segment per step, weighted by the step's
+    // duration (100-MHz clock): counters[24..28] = sum dt, sum active * dt, steps, sum active, waves
+    unsigned long long d_dt = 0, d_adt = 0, d_steps = 0, d_act = 0;
+    uint64_t d_t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t d_a = 0;
+#endif
     for (;;) {
         bool got;
         pool_refill(P, pool_n, priv, pn, !have, got, cur, link, pix);
         have = have || got;
-        if (__ballot(have) == 0ull) break;
+#ifdef TRT_DIAG_PASSA_STEPS
+        {
+            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            if (d_steps) {
+                d_dt += t - d_t0;
+                d_adt += (t - d_t0) * d_a;
+            }
+            d_t0 = t;
+            d_a = (uint32_t)__popcll(__ballot(have));
+            if (d_a) {
+                ++d_steps;
+                d_act += d_a;
+            }
+        }
+#endif
+        if (__ballot(have) == 0ull) {
+#ifdef TRT_DIAG_PASSA_STEPS
+            if (lane_id() == 0u) {
+                atomicAdd(&A.counters[24], d_dt);
+                atomicAdd(&A.counters[25], d_adt);
+                atomicAdd(&A.counters[26], d_steps);
+                atomicAdd(&A.counters[27], d_act);
+                atomicAdd(&A.counters[28], 1ull);
+            }
+#endif
+            break;
+        }
         // every lane takes this step's slot, working or not: the lanes stay on one row of one
         // chunk (one chunk per kEvRows steps of the wave, coalesced event stores); idle lanes'
         // slots stay unused
@@ -2470,220 +2489,6 @@ __global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void 
     if (COUNT) flush_counts(A, cnt);
 }
 
-// ---- single-frame launches of triangle-free frames: subtree hand-off (KArgs::share) ---------
-//
-// A single-frame launch (the reference's drawFrame pacing: one dispatch per frame, main.cpp:2181-
-// 2205) lasts as long as its slowest wave, and in a C2 frame that is a glass tile whose pixels
-// each walk a 15-segment tree one segment after the other, every miss a dependent envmap gather
-// (31 us launch, its longest tile 26 us: profiles/r05t_clock_c2_single_frame.log) while the lanes
-// of the tile's cheap pixels idle.  Here a lane whose own pixel is finished helps: when an owner
-// lane makes both children, it continues with the reflection child (the reference pops it
-// first) and offers the refraction child's whole subtree in a slot of the wave's LDS pool; an
-// idle lane takes it, traces that subtree depth first exactly as the owner would (same DFS, same
-// arithmetic) and records its colour terms in order in the slot.  The owner keeps a placeholder
-// where the child would sit on its stack; when it pops it, it folds the recorded terms into its
-// running sum in order (the same additions: the refraction subtree is the contiguous run of the
-// pixel's pop order that follows the reflection subtree, shader.comp:530-575), or takes the
-// subtree back if no lane picked it up yet, or waits for the helper.  Bit-identical to the
-// per-pixel loop.  Helpers do not hand off further; a subtree of depth D - depth(child) <= 3 (at
-// most kShareTerms terms) is offered, so D <= 4 frames offer every refraction child.
-constexpr int kShareSlots = 32;
-constexpr int kShareTerms = 7;
-constexpr int kShareSlotFloats = 8 + 3 * kShareTerms + 1; // segment, terms, term count
-#ifndef TRT_SHARE_WAVES
-#define TRT_SHARE_WAVES 4
-#endif
-
-__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, 64);
-    return v;
-}
-
-// One segment of the per-pixel loop (cast_seg's GEOM 0 shading, through the factored helpers the
-// deferred passes use — the same operations in the same order): its colour term and children.
-__device__ __forceinline__ f3 share_segment(const KArgs& A, const Seg& cur, int D, float4* slab, Seg& refr,
-                                            bool& mk_refr, Seg& refl, bool& mk_refl) {
-    Cnt cnt;
-    Hit h;
-    scene_intersect<false, 0>(A, cur.o, cur.d, h, cnt, slab);
-    mk_refr = mk_refl = false;
-    if (h.kind == HIT_NONE) return muls(background(A, cur.d), cur.thr);
-    const Surf s = resolve_hit<false>(A, cur, h, cnt);
-    const f3 v = neg(cur.d), kdv = mk(s.kd[0], s.kd[1], s.kd[2]);
-    f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const LightTerm t = light_term(A, s, v, i);
-        if (!t.matters) continue;
-        if (shadow_intersect<false, 0>(A, t.so, t.ld, t.dist, cnt, slab)) continue;
-        diffuse = add(diffuse, muls(kdv, t.diff));
-        specular = add(specular, muls(kdv, t.spec));
-    }
-    make_children(cur, s, D, refr, mk_refr, refl, mk_refl);
-    return muls(add(muls(diffuse, s.alb[0]), muls(specular, s.alb[1])), cur.thr);
-}
-
-template <int CAP>
-__global__ __launch_bounds__(64, TRT_SHARE_WAVES) void share_kernel(KArgs A) {
-    static_assert(CAP >= 1 && CAP <= LDS_STACK_MAX, "the LDS segment stack");
-    __shared__ float lds[lds_stack_floats<CAP, 0, false>()];
-    __shared__ float pool_[kShareSlots * kShareSlotFloats];
-    __shared__ float4 slab[1];
-    lds_f32* P = (lds_f32*)pool_;
-    const uint32_t lane = lane_id();
-    const uint32_t tile = xcd_tile(A, blockIdx.x);
-    if (tile >= A.ntiles) return;
-    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u), k = (tile / A.ntx) * 8u + (lane >> 3);
-    const bool valid = x < A.width && k < A.rows;
-    const int D = (int)A.max_depth;
-    using Stk = DeferStack<CAP, true>;
-    typename Stk::Mem stk_mem;
-    Stk stk(lds, stk_mem);
-    enum : int { IDLE = 0, OWN = 1, HELP = 2 };
-    int mode = valid ? OWN : IDLE;
-    bool have = valid; // the lane holds `cur`
-    const f3 orig = mk(A.fr[0].cam[0], A.fr[0].cam[1], A.fr[0].cam[2]);
-    Seg cur = valid ? Seg{orig, primary_dir(A, x, band_row(A, k), 0), 1.0f, 0} : Seg{orig, orig, 0.0f, 0};
-    f3 S = mk(0.0f, 0.0f, 0.0f); // the owner's running sum
-    uint32_t hslot = 0, hn = 0;  // a helper's slot and the terms it recorded
-    // wave-uniform slot states: free, pending (offered, not taken), done (terms recorded)
-    uint32_t free_m = 0xFFFFFFFFu, pend_m = 0u, done_m = 0u;
-    auto slot_seg = [&](uint32_t sl) {
-        const lds_f32* q = P + sl * kShareSlotFloats;
-        return Seg{mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6], __float_as_int(q[7])};
-    };
-    for (;;) {
-        wave_lds_sync();
-        // 1. helpers without a segment: their subtree's next one, or the subtree is done
-        uint32_t done_now = 0u;
-        if (mode == HELP && !have) {
-            if (stk.n > 0) {
-                cur = stk.pop();
-                have = true;
-            } else {
-                P[hslot * kShareSlotFloats + 8 + 3 * kShareTerms] = __uint_as_float(hn);
-                done_now = 1u << hslot;
-                mode = IDLE;
-            }
-        }
-        if (__ballot(done_now != 0u)) {
-            wave_lds_sync(); // the term counts land before an owner reads them
-            done_m |= __builtin_amdgcn_readfirstlane(wave_or(done_now));
-        }
-        // 2. owners without a segment: pop (a placeholder: take it back, fold it, or wait)
-        uint32_t freed = 0u, taken = 0u;
-        if (mode == OWN && !have) {
-            for (int guard = 0; guard <= CAP; ++guard) {
-                if (stk.n == 0) { // the pixel's tree is done (shader.comp:582, 598-601)
-                    store_pixel(A, A.fr[0], (size_t)k * A.width + x, mk(clamp01(S.x), clamp01(S.y), clamp01(S.z)));
-                    mode = IDLE;
-                    break;
-                }
-                const Seg top = lds_get(stk.base + (stk.n - 1) * 8 * 64);
-                if (top.depth >= 0) {
-                    cur = stk.pop();
-                    have = true;
-                    break;
-                }
-                const uint32_t sl = (uint32_t)(-top.depth - 1);
-                if ((pend_m >> sl) & 1u) { // nobody took it: trace it here
-                    (void)stk.pop();
-                    cur = slot_seg(sl);
-                    have = true;
-                    taken |= 1u << sl;
-                    freed |= 1u << sl;
-                    break;
-                }
-                if (!((done_m >> sl) & 1u)) break; // a helper is still on it: wait
-                (void)stk.pop();
-                const lds_f32* q = P + sl * kShareSlotFloats;
-                const uint32_t n = __float_as_uint(q[8 + 3 * kShareTerms]);
-                for (uint32_t i = 0; i < n; ++i) S = add(S, mk(q[8 + 3 * i], q[9 + 3 * i], q[10 + 3 * i]));
-                freed |= 1u << sl;
-            }
-        }
-        if (__ballot(freed != 0u)) {
-            const uint32_t f = __builtin_amdgcn_readfirstlane(wave_or(freed));
-            const uint32_t t = __builtin_amdgcn_readfirstlane(wave_or(taken));
-            free_m |= f;
-            done_m &= ~f;
-            pend_m &= ~t;
-        }
-        // 3. idle lanes take the offered subtrees (by rank)
-        uint64_t im = __ballot(mode == IDLE);
-        while (im != 0ull && pend_m != 0u) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(im), sl = (uint32_t)__builtin_ctz(pend_m);
-            if (lane == l) {
-                mode = HELP;
-                hslot = sl;
-                hn = 0u;
-                cur = slot_seg(sl);
-                have = true;
-            }
-            im &= im - 1ull;
-            pend_m &= pend_m - 1u;
-        }
-        if (__ballot(have) == 0ull) break; // no lane holds work, so no owner waits either
-        // 4. one segment on every lane that holds one
-        bool offer = false;
-        Seg refr;
-        if (have) {
-            Seg refl;
-            bool mk_refr, mk_refl;
-            const f3 X = share_segment(A, cur, D, slab, refr, mk_refr, refl, mk_refl);
-            if (mode == OWN) {
-                S = add(S, X);
-            } else if (hn < (uint32_t)kShareTerms) {
-                lds_f32* q = P + hslot * kShareSlotFloats + 8 + 3 * hn;
-                q[0] = X.x;
-                q[1] = X.y;
-                q[2] = X.z;
-                ++hn;
-            }
-            have = false;
-            if (mk_refl) {
-                if (mk_refr) {
-                    if (mode == OWN && D - refr.depth <= 3) offer = true;
-                    else stk.push(refr);
-                }
-                cur = refl;
-                have = true;
-            } else if (mk_refr) {
-                cur = refr;
-                have = true;
-            }
-        }
-        // 5. offers: a free slot each (rank order), else the child goes on the owner's stack
-        uint64_t om = __ballot(offer);
-        if (om != 0ull) {
-            wave_lds_sync(); // this step's slot reads are done before a freed slot is rewritten
-            while (om != 0ull) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(om);
-                const bool ok = free_m != 0u;
-                const uint32_t sl = ok ? (uint32_t)__builtin_ctz(free_m) : 0u;
-                if (ok) {
-                    free_m &= free_m - 1u;
-                    pend_m |= 1u << sl;
-                }
-                if (lane == l) {
-                    if (ok) {
-                        lds_f32* q = P + sl * kShareSlotFloats;
-                        q[0] = refr.o.x; q[1] = refr.o.y; q[2] = refr.o.z;
-                        q[3] = refr.d.x; q[4] = refr.d.y; q[5] = refr.d.z;
-                        q[6] = refr.thr;
-                        q[7] = __int_as_float(refr.depth);
-                        stk.push(Seg{refr.o, refr.d, 0.0f, -(int)sl - 1}); // the placeholder
-                    } else {
-                        stk.push(refr);
-                    }
-                }
-                om &= om - 1ull;
-            }
-        }
-    }
-}
-
 // One round of a split frame: persistent waves take 64 tasks at a time (static schedule) from
 // the previous launch's queue, trace each task's subtree within the depth window (its
 // window-edge children go to the next queue) and add the subtree's colour to its pixel's
@@ -3026,14 +2831,6 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
                                  ? (A.nframes + 1u) / 2u
                                  : std::max(A.nframes, 1u);
     const dim3 fgrid(A.ntiles * fblocks);
-    // single-frame launch of a triangle-free frame: the subtree hand-off kernel (share_kernel)
-    if (!count && geom == 0 && A.share && A.nframes <= 1u && !A.spp_lanes && A.spp <= 1u && D >= 2u && D <= 5u) {
-        if (D == 2) hipLaunchKernelGGL(share_kernel<1>, grid, block, 0, stream, A);
-        else if (D == 3) hipLaunchKernelGGL(share_kernel<2>, grid, block, 0, stream, A);
-        else if (D == 4) hipLaunchKernelGGL(share_kernel<3>, grid, block, 0, stream, A);
-        else hipLaunchKernelGGL(share_kernel<4>, grid, block, 0, stream, A);
-        return hipGetLastError();
-    }
 #define TRT_LAUNCH_G(CAP, G)                                                                             \
     do {                                                                                                 \
         if (count) hipLaunchKernelGGL((trace_kernel<CAP, true, G, false>), fgrid, block, 0, stream, A);  \
