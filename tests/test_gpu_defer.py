@@ -10,6 +10,8 @@ Pixels whose event log does not fit (tiny capacities forced through the test hoo
 TRT_DEFER_EVCAP / TRT_DEFER_QCAP) are re-traced in place and must not change a bit either."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -268,4 +270,44 @@ def test_auto_in_flight_drops_a_slot_that_runs_out_of_memory(scenes, monkeypatch
             r.render_frames(p, out, 6, frame_stride=p.height * p.width * 4)
     finally:
         monkeypatch.delenv("TRT_TEST_FAIL_DEFER_SLOT", raising=False)
+        r.close()
+
+
+@pytest.mark.parametrize("group,inflight", [(2, 0), (3, 2), (4, 4), (8, 1), (16, 0)])
+def test_deferred_frame_groups(scenes, group, inflight):
+    """TRT_DEFER_GROUP: consecutive deferred frames of a frame loop traced by one launch sequence
+    (pass A over every frame's tiles, one pass B and one pass C over all of them, each frame with
+    its own scratch).  Ragged groups (the loop's last group is shorter), groups in flight and
+    both scenes: every frame equals the single deferred frame of its UBO bit for bit."""
+    import vkcomputeshader_tinyraytracer_amd as trt
+
+    old = os.environ.get("TRT_DEFER_GROUP")
+    os.environ["TRT_DEFER_GROUP"] = str(group)
+    try:
+        r = trt.Renderer(0)
+    finally:
+        if old is None:
+            os.environ.pop("TRT_DEFER_GROUP", None)
+        else:
+            os.environ["TRT_DEFER_GROUP"] = old
+    try:
+        for name in ("ref", "readme"):
+            sc = scenes[name]
+            r.upload_scene(sc)
+            p = sc.params()
+            n = 2 * group + 1
+            ubos = np.stack(S.camera_path(sc.ubo, n))
+            out = torch.zeros((n, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            r.set_deferred_shadows(DEFER_ON)
+            r.set_frames_in_flight(inflight)
+            r.render_frames(p, out, n, ubos=ubos, frame_stride=p.height * p.width * 4)
+            torch.cuda.synchronize()
+            r.set_frames_in_flight(0)
+            got = out.cpu().numpy()
+            for i in range(n):
+                r.update_ubo(ubos[i])
+                one, _ = _frame(r, sc, DEFER_ON)
+                assert np.array_equal(got[i], one), (name, i)
+    finally:
         r.close()

@@ -102,3 +102,18 @@ def test_c4_whole_frame():
         assert gst[k] == ost[k], (k, gst[k], ost[k])
     assert_rgba8_close(g8, o8)
     assert (g8b == g8).all()
+
+
+def test_c5_90_spread_rows(gpu_renderer):
+    """A wider C5 check (round 6): every 24th full-width row of the 3840x2160 frame at 16
+    jittered spp — 90 rows (4.2 % of the frame), ~1 minute of the oracle on the box's share."""
+    sc = S.CONFIGS["C5"]()
+    p = sc.params()
+    p.band_rows, p.band_count, p.band_index = 1, 24, 11
+    gpu_renderer.upload_scene(sc)
+    g8, _, gst = gpu_renderer.draw_frame(p, count=True)
+    o8, _, ost = orc.render(sc, p, threads=0)
+    assert g8.shape == o8.shape == (90, p.width, 4)
+    for k in T.Stats.EXACT:
+        assert gst[k] == ost[k], (k, gst[k], ost[k])
+    assert_rgba8_close(g8, o8)

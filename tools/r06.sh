@@ -62,6 +62,23 @@ for stage in "$@"; do
       done
     done
     python tools/ab_summary.py "$OUT/ab.jsonl" ;;
+  groups) # deferred frame groups (TRT_DEFER_GROUP = G frames per launch, N groups in flight)
+    for round in 1 2; do
+      for gn in "1 16" "2 8" "4 4" "8 2" "16 1"; do
+        set -- $gn
+        for cfg in ref readme; do
+          TRT_DEFER_GROUP=$1 timeout -k 10 300 python tools/kbench.py --config $cfg --frames 192 --inflight $2 \
+            --tag "g$1n$2:$cfg" >> "$OUT/groups.jsonl" 2>> "$OUT/groups.err" || { tail -5 "$OUT/groups.err"; exit 1; }
+        done
+      done
+    done
+    python tools/ab_summary.py "$OUT/groups.jsonl"
+    for gn in "1 0" "4 4" "8 2" "16 1"; do # the C++ host at HIP's default queue count
+      set -- $gn
+      env -u GPU_MAX_HW_QUEUES TRT_DEFER_GROUP=$1 timeout -k 10 200 tests/native/drop_in_host --bench \
+        tests/golden/dropin_meshes.bin 192 "$2" >> "$OUT/groups_cabi.log" 2>&1 || exit 1
+    done
+    grep bench "$OUT/groups_cabi.log" ;;
   cabi) # the shipped frame through the C++ host: HIP's default queues (auto / 4 in flight), 32 queues
     for cf in "unset 0" "unset 4" "unset 2" "32 0"; do
       set -- $cf

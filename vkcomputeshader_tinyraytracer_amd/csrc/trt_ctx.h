@@ -67,6 +67,12 @@ struct trt_ctx {
     int frame_group = -1; // TRT_FRAME_GROUP (1 or 2); -1 = auto: 2 for triangle-free scenes, else 1
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     uint32_t defer_in_flight = 16; // auto frames in flight of deferred-shadow loops (TRT_DEFER_IN_FLIGHT env)
+    // frames per deferred launch group of a frame loop: TRT_DEFER_GROUP env, 0 = auto (by the
+    // hardware queues: render_frame_list)
+    uint32_t defer_group = 0;
+    // hardware queues HIP gives this process: GPU_MAX_HW_QUEUES at trt_create (HIP's default 4
+    // when unset); the library only reads it
+    uint32_t hw_queues = 4;
     int subtree_split = TRT_SPLIT_AUTO;
     int deferred_shadows = TRT_DEFER_AUTO;
     // pass-A waves per tile of a deferred frame: 0 = auto (2 when <= 4 frames overlap, else 1),
@@ -93,6 +99,7 @@ struct trt_ctx {
         uint32_t* fb = nullptr;
         trt::DeferCtr* dctr = nullptr;
         size_t ev_chunks = 0, shq_cap = 0, dnpx = 0;
+        uint32_t dframes = 0; // frames the deferred scratch holds (a launch group), each of the sizes above
         // per-stripe capacities the slot's last deferred frame ran with (trt_defer_stats)
         size_t used_ev_cap = 0, used_shq_cap = 0;
         // The stream of the slot's last frame and an event after it: a frame on another

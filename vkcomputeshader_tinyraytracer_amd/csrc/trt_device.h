@@ -246,6 +246,11 @@ struct KArgs {
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
     uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4: trace_tile)
+    // frames of a deferred launch (trt_render_frames groups consecutive frames): frame f's
+    // scratch is ev + f * ev_fstride, shq + f * shq_fstride, px_ev / fb + f * px_fstride, dctr + f
+    uint32_t dframes;
+    uint32_t px_fstride;
+    size_t ev_fstride, shq_fstride;
     uint32_t spp_lanes;               // spp > 1: one lane per sample (trace_samples), spp waves per tile
     FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch
 };

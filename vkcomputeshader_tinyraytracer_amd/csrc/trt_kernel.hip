@@ -1371,7 +1371,22 @@ __device__ __forceinline__ float from_fixed(unsigned long long v) {
 }
 
 // ---- deferred shadows: the per-lane event pool (trt_device.h kEvRows) --------------------
+// One frame's deferred scratch (a deferred launch traces A.dframes frames, each with its own
+// event pool, query queue, per-pixel roots, fallback list and counters: frame f's are the bases
+// in KArgs plus f times the per-frame strides).  Wave-uniform.
+struct DScratch {
+    float4* ev;
+    float4* shq;
+    uint2* px_ev;
+    uint32_t* fb;
+    DeferCtr* dctr;
+};
+__device__ __forceinline__ DScratch dscratch(const KArgs& A, uint32_t f) {
+    return DScratch{A.ev + f * A.ev_fstride, A.shq + f * A.shq_fstride, A.px_ev + (size_t)f * A.px_fstride,
+                    A.fb + (size_t)f * A.px_fstride, A.dctr + f};
+}
 struct EvLog {
+    DScratch S;          // the frame's scratch
     uint32_t stripe = 0; // the stripe of the event pool and query queue (wave-uniform)
     uint32_t k = 0;      // events this lane has logged
     uint32_t chunk = 0;  // the chunk holding event k - 1
@@ -1389,7 +1404,7 @@ __device__ __forceinline__ uint32_t ev_alloc(const KArgs& A, EvLog& L) {
     if (m) {
         const int leader = __ffsll((unsigned long long)m) - 1;
         uint32_t base = 0;
-        if ((int)lane_id() == leader) base = atomicAdd(&A.dctr->chunks[L.stripe * kCtrStride], 1u);
+        if ((int)lane_id() == leader) base = atomicAdd(&L.S.dctr->chunks[L.stripe * kCtrStride], 1u);
         base = __shfl(base, leader, 64);
         if (need) {
             if (base >= A.ev_cap) L.ovf = true;
@@ -1400,8 +1415,8 @@ __device__ __forceinline__ uint32_t ev_alloc(const KArgs& A, EvLog& L) {
     return (L.chunk * kEvRows + row) * 64u + lane_id();
 }
 // Plane p (0..3) of event slot s = (chunk * kEvRows + row) * 64 + lane.
-__device__ __forceinline__ float4* ev_plane(const KArgs& A, uint32_t s, uint32_t p) {
-    return A.ev + ((size_t)(s >> 6) * 4u + p) * 64u + (s & 63u);
+__device__ __forceinline__ float4* ev_plane(float4* ev, uint32_t s, uint32_t p) {
+    return ev + ((size_t)(s >> 6) * 4u + p) * 64u + (s & 63u);
 }
 
 // The closest hit's shading inputs (shader.comp:302-360): point, normal, material.
@@ -1867,8 +1882,8 @@ __device__ __forceinline__ PSeg pool_get(const lds_f32* P, uint32_t e) {
 
 // A pixel whose log does not fit (event pool, query queue or task queue full) is re-traced in
 // place by defer_fallback: its tree root becomes kEvNone and it is listed once.
-__device__ __forceinline__ void defer_mark_fallback(const KArgs& A, uint32_t pix) {
-    if (atomicExch(&A.px_ev[pix].x, kEvNone) != kEvNone) A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
+__device__ __forceinline__ void defer_mark_fallback(const DScratch& S, uint32_t pix) {
+    if (atomicExch(&S.px_ev[pix].x, kEvNone) != kEvNone) S.fb[atomicAdd(&S.dctr->nfb, 1u)] = pix;
 }
 
 // One traced segment of pass A: its event (slot `slot`, linked to `link` of pixel `pix`), its
@@ -1881,21 +1896,22 @@ __device__ __forceinline__ void defer_shade(const KArgs& A, EvLog& L, uint32_t s
     const int D = (int)A.max_depth;
     Cnt cnt;
     have = false;
+    const DScratch& S = L.S;
     if (L.ovf && link == kEvRoot) { // no event this frame yet: list the pixel
-        atomicExch(&A.px_ev[pix].x, kEvNone);
-        A.fb[atomicAdd(&A.dctr->nfb, 1u)] = pix;
+        atomicExch(&S.px_ev[pix].x, kEvNone);
+        S.fb[atomicAdd(&S.dctr->nfb, 1u)] = pix;
         return;
     }
     if (L.ovf) {
-        defer_mark_fallback(A, pix);
+        defer_mark_fallback(S, pix);
         return;
     }
     // where this segment's event lives: the pixel's root, or its parent's child link
-    if (link == kEvRoot) atomicExch(&A.px_ev[pix].x, slot);
-    else reinterpret_cast<uint32_t*>(ev_plane(A, link >> 1, 3))[2u + (link & 1u)] = slot;
+    if (link == kEvRoot) atomicExch(&S.px_ev[pix].x, slot);
+    else reinterpret_cast<uint32_t*>(ev_plane(S.ev, link >> 1, 3))[2u + (link & 1u)] = slot;
     if (h.kind == HIT_NONE) {
         const f3 c = muls(background(A, cur.d), cur.thr);
-        *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst));
+        *ev_plane(S.ev, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst));
         return;
     }
     const Surf s = resolve_hit<false>(A, cur, h, cnt);
@@ -1911,11 +1927,11 @@ __device__ __forceinline__ void defer_shade(const KArgs& A, EvLog& L, uint32_t s
         const uint64_t m = __ballot(true);
         const int leader = __ffsll((unsigned long long)m) - 1;
         uint32_t base = 0;
-        if ((int)lane_id() == leader) base = atomicAdd(&A.dctr->nq[L.stripe * kCtrStride], (uint32_t)__popcll(m));
+        if ((int)lane_id() == leader) base = atomicAdd(&S.dctr->nq[L.stripe * kCtrStride], (uint32_t)__popcll(m));
         base = __shfl(base, leader, 64);
         const uint32_t qi = base + lane_rank(m);
         if (qi < A.shq_cap) {
-            float4* q = A.shq + 2 * ((size_t)L.stripe * A.shq_cap + qi);
+            float4* q = S.shq + 2 * ((size_t)L.stripe * A.shq_cap + qi);
             q[0] = make_float4(t.so.x, t.so.y, t.so.z, t.dist);
             q[1] = make_float4(t.ld.x, t.ld.y, t.ld.z, __uint_as_float((slot << 2) | (uint32_t)i));
             qmask |= 1u << i;
@@ -1938,18 +1954,18 @@ __device__ __forceinline__ void defer_shade(const KArgs& A, EvLog& L, uint32_t s
         mk_refl = mk_refr = false;
     }
     if (L.ovf) {
-        defer_mark_fallback(A, pix);
+        defer_mark_fallback(S, pix);
         return;
     }
     if (qmask == 0u) { // no light can add anything: the colour term is known now
         f3 diffuse = mk(0.0f, 0.0f, 0.0f), specular = mk(0.0f, 0.0f, 0.0f);
         const f3 c = muls(add(muls(diffuse, s.alb[0]), muls(specular, s.alb[1])), cur.thr);
-        *ev_plane(A, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst | kids));
+        *ev_plane(S.ev, slot, 0) = make_float4(c.x, c.y, c.z, __uint_as_float(kEvTagConst | kids));
     } else { // pass B ORs the occluded lights into plane 3's second word
-        *ev_plane(A, slot, 0) = make_float4(s.kd[0], s.kd[1], s.kd[2], __uint_as_float(qmask | kids));
-        *ev_plane(A, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], s.alb[0]);
-        *ev_plane(A, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], s.alb[1]);
-        *reinterpret_cast<float2*>(ev_plane(A, slot, 3)) = make_float2(cur.thr, 0.0f);
+        *ev_plane(S.ev, slot, 0) = make_float4(s.kd[0], s.kd[1], s.kd[2], __uint_as_float(qmask | kids));
+        *ev_plane(S.ev, slot, 1) = make_float4(dterm[0], dterm[1], dterm[2], s.alb[0]);
+        *ev_plane(S.ev, slot, 2) = make_float4(sterm[0], sterm[1], sterm[2], s.alb[1]);
+        *reinterpret_cast<float2*>(ev_plane(S.ev, slot, 3)) = make_float2(cur.thr, 0.0f);
     }
     // continue with the reflection child (the reference pops it first; here it keeps the lane
     // on nearby rays), offer the refraction child to the wave
@@ -2177,7 +2193,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& A, const FrameRec& F, s
 // cheap tiles.
 template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool DEFER = false, bool HYB = SPLIT>
 __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, uint32_t tile, Cnt& cnt, float* lds,
-                                           float4* slab, uint32_t sub = 0) {
+                                           float4* slab, uint32_t sub = 0, uint32_t frame = 0) {
     const uint32_t lane = lane_id();
     if (tile >= A.ntiles) return;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
@@ -2189,6 +2205,7 @@ __device__ __forceinline__ void trace_tile(const KArgs& A, const FrameRec& F, ui
         k = (tile / A.ntx) * 8u + sub * rows + (lane >> 3);
         const bool valid = x < A.width && k < A.rows && (lane >> 3) < rows;
         EvLog L;
+        L.S = dscratch(A, frame); // this frame's scratch (frame `frame` of the launch)
         // multiplicative hash of the tile: a frame's costly region (a glass object) spans few
         // tile columns, so tile % stripes would pile its queries into a few stripes
         L.stripe = ((tile * S + sub) * 0x9E3779B1u) >> (32 - 7);
@@ -2462,9 +2479,12 @@ __global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void 
             t = vb - f * A.ntiles;
             tile = xcd_tile(A, t, f);
         }
-    } else if (DEFER && !SPLIT && A.defer_sub > 1u) { // defer_sub waves per tile (trace_tile)
-        tile = xcd_tile(A, t / A.defer_sub);
-        trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % A.defer_sub);
+    } else if (DEFER && !SPLIT) { // defer_sub waves per tile of each of dframes frames (trace_tile)
+        const uint32_t Sd = A.defer_sub > 1u ? A.defer_sub : 1u, per = A.ntiles * Sd;
+        f = vb / per;
+        t = vb - f * per;
+        tile = xcd_tile(A, t / Sd);
+        trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % Sd, f);
         return;
     } else {
         tile = xcd_tile(A, t);
@@ -2520,6 +2540,7 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void trace_tasks(KArgs 
                 link = A.q_link_in[t];
             }
             EvLog L;
+            L.S = dscratch(A, 0u); // split launches trace one frame
             // wave-uniform (ev_alloc and the query appends reserve from one stripe per wave)
             L.stripe = ((base / 64u + 0x5bd1e995u * A.split_d1) * 0x9E3779B1u) >> (32 - 7);
             defer_walk<GEOM, true>(A, lds, slab, L, valid, root, link, pixel);
@@ -2582,22 +2603,25 @@ static void launch_split(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
 // order is free), 64 consecutive queries of one stripe per wave step — every lane of a wave
 // runs a query, where in the per-pixel loop a wave runs the shadow rays of whichever of its
 // lanes sit at a hit.  Static schedule: wave w takes stripe w % kDeferStripes and every
-// (gridDim / kDeferStripes)-th 64-query block of it.  An occluded query ORs its light's bit
-// into its event.
+// (blocks per frame / kDeferStripes)-th 64-query block of it.  An occluded query ORs its
+// light's bit into its event.  A launch of dframes frames gives each frame gridDim / dframes
+// blocks (a multiple of kDeferStripes).
 template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
-    const uint32_t s = blockIdx.x % kDeferStripes, K = gridDim.x / kDeferStripes;
-    const uint32_t n = min(A.dctr->nq[s * kCtrStride], A.shq_cap);
-    const float4* Q = A.shq + 2 * (size_t)s * A.shq_cap;
-    for (uint32_t base = (blockIdx.x / kDeferStripes) * 64u; base < n; base += K * 64u) {
+    const uint32_t per = gridDim.x / max(A.dframes, 1u), f = blockIdx.x / per, b = blockIdx.x - f * per;
+    const DScratch S = dscratch(A, f);
+    const uint32_t s = b % kDeferStripes, K = per / kDeferStripes;
+    const uint32_t n = min(S.dctr->nq[s * kCtrStride], A.shq_cap);
+    const float4* Q = S.shq + 2 * (size_t)s * A.shq_cap;
+    for (uint32_t base = (b / kDeferStripes) * 64u; base < n; base += K * 64u) {
         const uint32_t i = base + threadIdx.x;
         if (i < n) {
-            const float4 a = Q[2 * (size_t)i], b = Q[2 * (size_t)i + 1];
-            if (shadow_intersect<false, GEOM>(A, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), a.w, cnt, slab)) {
-                const uint32_t t = __float_as_uint(b.w);
-                atomicOr(reinterpret_cast<uint32_t*>(ev_plane(A, t >> 2, 3)) + 1, 1u << (t & 3u));
+            const float4 a = Q[2 * (size_t)i], q = Q[2 * (size_t)i + 1];
+            if (shadow_intersect<false, GEOM>(A, mk(a.x, a.y, a.z), mk(q.x, q.y, q.z), a.w, cnt, slab)) {
+                const uint32_t t = __float_as_uint(q.w);
+                atomicOr(reinterpret_cast<uint32_t*>(ev_plane(S.ev, t >> 2, 3)) + 1, 1u << (t & 3u));
             }
         }
     }
@@ -2607,14 +2631,15 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArg
 // a segment, then its reflection subtree, then its refraction subtree) with exactly cast_seg's
 // arithmetic (a lit light's kd * diffuse / kd * specular terms added in light order, then
 // colour += thr * (diffuse * albedo.x + specular * albedo.y)); then clamp, gamma and the dual
-// store.  Lane = the pixel's lane in its pass-A tile.
+// store.  Lane = the pixel's lane in its pass-A tile; block f * ntiles + tile: frame f.
 __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
-    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    const uint32_t f = blockIdx.x / A.ntiles, tile = blockIdx.x - f * A.ntiles, lane = threadIdx.x;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;
+    const DScratch S = dscratch(A, f);
     const size_t o = (size_t)k * A.width + x;
-    const uint32_t root = A.px_ev[o].x;
+    const uint32_t root = S.px_ev[o].x;
     if (root == kEvNone) return; // defer_fallback's pixel
     f3 color = mk(0.0f, 0.0f, 0.0f);
     uint32_t stk[kMaxTreeDepth]; // pending refraction subtrees, one per depth of the path
@@ -2622,20 +2647,20 @@ __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
     for (;;) {
         // a tree has at most 2^MAX_DEPTH - 1 events: a corrupt log must not hang the GPU
         if (++steps > (1u << kMaxTreeDepth) || s >= A.ev_cap * kDeferStripes * kEvRows * 64u) {
-            if (atomicCAS(&A.dctr->pad[0], 0u, 1u) == 0u) {
-                uint32_t* d = A.dctr->pad;
+            if (atomicCAS(&S.dctr->pad[0], 0u, 1u) == 0u) {
+                uint32_t* d = S.dctr->pad;
                 d[1] = (uint32_t)o; d[2] = root; d[3] = s; d[4] = sp; d[5] = steps;
             }
             color = mk(1.0f, 0.0f, 1.0f);
             break;
         }
-        const float4 p0 = *ev_plane(A, s, 0);
+        const float4 p0 = *ev_plane(S.ev, s, 0);
         const uint32_t tag = __float_as_uint(p0.w);
-        const float4 p3 = *ev_plane(A, s, 3);
+        const float4 p3 = *ev_plane(S.ev, s, 3);
         if (tag & kEvTagConst) {
             color = add(color, mk(p0.x, p0.y, p0.z));
         } else {
-            const float4 p1 = *ev_plane(A, s, 1), p2 = *ev_plane(A, s, 2);
+            const float4 p1 = *ev_plane(S.ev, s, 1), p2 = *ev_plane(S.ev, s, 2);
             const uint32_t lit = tag & 7u & ~__float_as_uint(p3.y);
             const f3 kdv = mk(p0.x, p0.y, p0.z);
             const float dterm[3] = {p1.x, p1.y, p1.z}, sterm[3] = {p2.x, p2.y, p2.z};
@@ -2660,7 +2685,7 @@ __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
             break;
         }
     }
-    store_pixel(A, A.fr[0], o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
+    store_pixel(A, A.fr[f], o, mk(clamp01(color.x), clamp01(color.y), clamp01(color.z)));
 }
 
 // Pixels whose log did not fit (event pool or query queue full) are traced again from scratch
@@ -2670,15 +2695,18 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_fallback(KAr
     __shared__ float lds[lds_stack_floats<CAP, GEOM, false>()];
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
-    const uint32_t n = A.dctr->nfb;
-    const f3 orig = mk(A.fr[0].cam[0], A.fr[0].cam[1], A.fr[0].cam[2]);
-    for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
-        const uint32_t i = base + threadIdx.x;
-        if (i < n) {
-            const uint32_t o = A.fb[i];
-            const uint32_t k = o / A.width, x = o % A.width;
-            const f3 c = cast_ray<CAP, false, GEOM>(A, orig, primary_dir(A, x, band_row(A, k), 0), cnt, lds, slab);
-            store_pixel(A, A.fr[0], o, c);
+    for (uint32_t f = 0; f < max(A.dframes, 1u); ++f) { // each frame of the launch, its list
+        const DScratch S = dscratch(A, f);
+        const uint32_t n = S.dctr->nfb;
+        const f3 orig = mk(A.fr[f].cam[0], A.fr[f].cam[1], A.fr[f].cam[2]);
+        for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+            const uint32_t i = base + threadIdx.x;
+            if (i < n) {
+                const uint32_t o = S.fb[i];
+                const uint32_t k = o / A.width, x = o % A.width;
+                const f3 c = cast_ray<CAP, false, GEOM>(A, orig, primary_dir(A, x, band_row(A, k), 0), cnt, lds, slab);
+                store_pixel(A, A.fr[f], o, c);
+            }
         }
     }
 }
@@ -2696,7 +2724,7 @@ template <int CAP, int GEOM, bool HYB>
 static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 block) {
     KArgs A = A0;
     const uint32_t stages = defer_stages();
-    const uint32_t D = A.max_depth, W = A.split_w;
+    const uint32_t D = A.max_depth, W = A.split_w, F = std::max(A.dframes, 1u);
     if (HYB && W >= 1 && W < D && A.ctr && A.q_link_buf[0]) {
         // subtree split: the tile kernel traces depths < W, each round the next window
         A.split_d1 = W;
@@ -2718,15 +2746,19 @@ static void launch_defer(const KArgs& A0, hipStream_t stream, dim3 grid, dim3 bl
                                dim3(64), 0, stream, A);
         }
     } else {
+        // dframes frames in one launch: ntiles * defer_sub blocks per frame
         const uint32_t S = A.defer_sub > 1u ? A.defer_sub : 1u;
-        hipLaunchKernelGGL((trace_kernel<0, false, GEOM, false, true, false>), dim3(grid.x * S), block, 0, stream, A);
+        hipLaunchKernelGGL((trace_kernel<0, false, GEOM, false, true, false>), dim3(grid.x * S * F), block, 0, stream, A);
     }
     // persistent: up to 8 waves per SIMD (the shadow-only kernel is light on VGPRs and LDS;
-    // waves that find the queue drained exit at once)
-    if (stages & 4)
-        hipLaunchKernelGGL(defer_shadows<GEOM>, dim3(((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes),
-                           dim3(64), 0, stream, A);
-    if (stages & 8) hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles), dim3(64), 0, stream, A);
+    // waves that find the queue drained exit at once); a frame group shares the grid (each frame
+    // a multiple of kDeferStripes blocks)
+    if (stages & 4) {
+        const uint32_t total = ((A.num_cus * 32 + kDeferStripes - 1) / kDeferStripes) * kDeferStripes;
+        const uint32_t per = std::max(kDeferStripes, (total / F / kDeferStripes) * kDeferStripes);
+        hipLaunchKernelGGL(defer_shadows<GEOM>, dim3(per * F), dim3(64), 0, stream, A);
+    }
+    if (stages & 8) hipLaunchKernelGGL(defer_resolve, dim3(A.ntiles * F), dim3(64), 0, stream, A);
     if (!(stages & 16)) return;
     // the fallback runs the per-pixel loop (deep frames: its full-depth private stack)
     if constexpr (HYB)
@@ -2781,7 +2813,7 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
     const dim3 grid(A.ntiles), block(64);
     const int geom = A.nbatch == 0 ? 0 : (A.bvh && !(A.flags & TRT_FLAG_BATCH_WALK)) ? (A.bvh_waves4 ? 3 : 2) : 1;
     if (A.defer && !count && A.spp <= 1 && A.dctr && A.ev && A.shq && A.px_ev && A.fb) {
-        hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr), stream);
+        hipError_t e = hipMemsetAsync(A.dctr, 0, sizeof(DeferCtr) * std::max(A.dframes, 1u), stream);
         if (e == hipSuccess && A.split_w >= 1 && A.ctr) e = hipMemsetAsync(A.ctr, 0, sizeof(SplitCtr), stream);
         if (e != hipSuccess) return e;
 #define TRT_DEFER_G(CAP, HYB)                                                \

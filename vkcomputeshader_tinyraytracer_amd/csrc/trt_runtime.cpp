@@ -228,6 +228,9 @@ int trt_create(trt_ctx** out, int hip_device) {
         const int ppw = std::atoi(e);
         c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
     }
+    if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) c->hw_queues = (uint32_t)std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("TRT_DEFER_GROUP"))
+        c->defer_group = (uint32_t)std::min((int)trt::kMaxLaunchFrames, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT"))
         c->defer_in_flight = (uint32_t)std::min((int)TRT_BUILD_MAX_IN_FLIGHT, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
@@ -736,29 +739,55 @@ DeferSizes defer_sizes(size_t ntiles, uint32_t D, size_t npx) {
     return z;
 }
 
-bool defer_bufs_fit(const trt_ctx::SplitBufs& b, const DeferSizes& z, size_t npx) {
-    return z.chunks <= b.ev_chunks && z.qcap <= b.shq_cap && npx <= b.dnpx;
+// A slot holds the scratch of `dframes` frames (a deferred launch group), each of the per-frame
+// capacities below.
+bool defer_bufs_fit(const trt_ctx::SplitBufs& b, const DeferSizes& z, size_t npx, uint32_t frames) {
+    return z.chunks <= b.ev_chunks && z.qcap <= b.shq_cap && npx <= b.dnpx && frames <= b.dframes;
 }
 
-// Device bytes one frames-in-flight slot needs for a deferred frame of these params (0 when
-// the slot already holds enough).
-size_t defer_slot_bytes(const trt_ctx* c, const trt_params* p, uint32_t slot) {
+// Deferred frame loop shape: `group` frames per launch sequence on each of `slots` in-flight
+// slots.  Explicit: TRT_DEFER_GROUP, or trt_set_frames_in_flight (then groups of 1, the
+// reference's pacing when it is 2).  Auto: about defer_in_flight (16) frames overlap in all,
+// spread over at most half the process's hardware queues — a stream per slot, and slots sharing
+// a queue serialise: with 32 queues 16 slots of 1 frame; with HIP's default 4 queues 2 slots of
+// 8 frames (the shipped frame through the C++ host 0.82 -> 0.55 ms per frame;
+// profiles/r06f_defer_groups_cabi_default_queues.log; at 32 queues groups of 2 / 4 / 8 tie / lose
+// 14 % / 25 %, profiles/r06f_ab_defer_groups.jsonl).
+void defer_shape(const trt_ctx* c, uint32_t& group, uint32_t& slots) {
+    const uint32_t T = std::max(c->defer_in_flight, 1u);
+    if (c->frames_in_flight) {
+        slots = c->frames_in_flight;
+        group = c->defer_group ? c->defer_group : 1u;
+        return;
+    }
+    if (c->defer_group) {
+        group = c->defer_group;
+        slots = std::max(1u, (T + group - 1) / group);
+        return;
+    }
+    slots = std::min(T, std::max(2u, c->hw_queues / 2u));
+    group = (T + slots - 1) / slots;
+}
+
+// Device bytes one frames-in-flight slot needs for a group of `frames` deferred frames of these
+// params (0 when the slot already holds enough).
+size_t defer_slot_bytes(const trt_ctx* c, const trt_params* p, uint32_t slot, uint32_t frames) {
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     const size_t ntiles = ((p->width + 7u) / 8u) * ((trt_output_rows(p) + 7u) / 8u);
     const DeferSizes z = defer_sizes(ntiles, p->max_depth, npx);
-    return defer_bufs_fit(c->split[slot], z, npx) ? 0 : z.bytes;
+    return defer_bufs_fit(c->split[slot], z, npx, frames) ? 0 : z.bytes * frames;
 }
 
 // The automatic frames-in-flight count of a deferred loop, bounded by device memory: each slot
 // holds its own scratch (defer_sizes: the shipped 1024x768 frame ~1 GB per slot), and the slots that would still need allocating may take
 // at most half of the free device memory.
-uint32_t fit_defer_slots(const trt_ctx* c, const trt_params* p, uint32_t want) {
+uint32_t fit_defer_slots(const trt_ctx* c, const trt_params* p, uint32_t want, uint32_t frames) {
     size_t freeb = 0, total = 0;
     if (hipMemGetInfo(&freeb, &total) != hipSuccess) return want;
     size_t need = 0;
     uint32_t n = 0;
     for (; n < want && n < TRT_BUILD_MAX_IN_FLIGHT; ++n) {
-        need += defer_slot_bytes(c, p, n);
+        need += defer_slot_bytes(c, p, n, frames);
         if (n > 0 && need > freeb / 2) break;
     }
     return std::max(1u, n);
@@ -767,11 +796,14 @@ uint32_t fit_defer_slots(const trt_ctx* c, const trt_params* p, uint32_t want) {
 void free_defer_bufs(trt_ctx::SplitBufs& b) {
     void* ps[] = {b.ev, b.shq, b.px_ev, b.fb};
     for (void* q : ps) (void)hipFree(q);
+    (void)hipFree(b.dctr);
     b.ev = nullptr;
     b.shq = nullptr;
     b.px_ev = nullptr;
     b.fb = nullptr;
+    b.dctr = nullptr;
     b.ev_chunks = b.shq_cap = b.dnpx = 0;
+    b.dframes = 0;
 }
 
 // Allocates slot `slot`'s deferred-frame scratch for this frame and fills
@@ -780,18 +812,19 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     auto& b = c->split[slot];
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     const DeferSizes z = defer_sizes(A.ntiles, p->max_depth, npx);
-    if (!defer_bufs_fit(b, z, npx)) {
+    const uint32_t G = std::max(A.nframes, 1u); // frames of this launch, each with its own scratch
+    if (!defer_bufs_fit(b, z, npx, G)) {
         free_defer_bufs(b);
         hipError_t e = hipSuccess;
         auto alloc = [&](void** q, size_t bytes) {
             if (e == hipSuccess && bytes) e = hipMalloc(q, bytes);
         };
         if ((int)slot == test_fail_defer_slot()) e = hipErrorOutOfMemory;
-        alloc((void**)&b.ev, z.chunks * kPoolEvBytes);
-        alloc((void**)&b.shq, z.qcap * 2 * sizeof(float4));
-        alloc((void**)&b.px_ev, npx * sizeof(uint2));
-        alloc((void**)&b.fb, npx * sizeof(uint32_t));
-        if (!b.dctr) alloc((void**)&b.dctr, sizeof(trt::DeferCtr));
+        alloc((void**)&b.ev, G * z.chunks * kPoolEvBytes);
+        alloc((void**)&b.shq, G * z.qcap * 2 * sizeof(float4));
+        alloc((void**)&b.px_ev, G * npx * sizeof(uint2));
+        alloc((void**)&b.fb, G * npx * sizeof(uint32_t));
+        alloc((void**)&b.dctr, G * sizeof(trt::DeferCtr));
         if (e != hipSuccess) {
             free_defer_bufs(b);
             return hip_fail(c, e, "alloc deferred-frame buffers");
@@ -799,6 +832,7 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
         b.ev_chunks = z.chunks;
         b.shq_cap = z.qcap;
         b.dnpx = npx;
+        b.dframes = G;
     }
     A.defer = 1;
     // pass-A waves per tile (pool design): explicit (TRT_DEFER_PPW), else by the frames that
@@ -806,7 +840,7 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     // segments — sets the rate, and two waves per tile halve that chain (the shipped frame at 2
     // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
     // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
-    A.defer_sub = c->defer_sub ? c->defer_sub : (c->cur_in_flight <= 4u ? 2u : 1u);
+    A.defer_sub = c->defer_sub ? c->defer_sub : (c->cur_in_flight * G <= 4u ? 2u : 1u);
     // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
     A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", z.chunks / trt::kDeferStripes);
     A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", z.qcap / trt::kDeferStripes);
@@ -815,6 +849,10 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     A.px_ev = b.px_ev;
     A.fb = b.fb;
     A.dctr = b.dctr;
+    A.dframes = G;
+    A.ev_fstride = b.ev_chunks * (kPoolEvBytes / sizeof(float4));
+    A.shq_fstride = b.shq_cap * 2;
+    A.px_fstride = (uint32_t)b.dnpx;
     b.used_ev_cap = A.ev_cap;
     b.used_shq_cap = A.shq_cap;
     return TRT_OK;
@@ -953,8 +991,16 @@ int render_frame_list(trt_ctx* c, const trt_params* p, const FrameOut* frames, u
     // 8, profiles/r02_ab_queues_deep.log).
     uint32_t want = c->frames_in_flight ? c->frames_in_flight : plain ? 1u : defer ? c->defer_in_flight : 4u;
     // auto: no more deferred slots than device memory holds (each slot owns its scratch)
-    if (!c->frames_in_flight && defer) want = fit_defer_slots(c, p, want);
-    const uint32_t cap = plain ? (c->frame_batch ? c->frame_batch : trt::kMaxLaunchFrames) : 1u;
+    // deferred frames (not split) go out in groups of frames per launch sequence (defer_shape)
+    uint32_t group = 1;
+    if (defer && !split) {
+        uint32_t slots = want;
+        defer_shape(c, group, slots);
+        group = std::min(group, trt::kMaxLaunchFrames);
+        want = slots;
+    }
+    if (!c->frames_in_flight && defer) want = fit_defer_slots(c, p, want, group);
+    const uint32_t cap = plain ? (c->frame_batch ? c->frame_batch : trt::kMaxLaunchFrames) : group;
     const uint32_t per_launch = std::max(1u, std::min(cap, (nframes + want - 1) / want));
     // launches: runs of consecutive frames sharing every UBO field but camPos
     std::vector<uint32_t> first{0};
