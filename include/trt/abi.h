@@ -155,7 +155,9 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * the README scene -28 %, profiles/r04z_ab_deferred_in_flight.jsonl).  Each slot is a HIP stream, so the process
  * needs as many hardware queues: the library leaves GPU_MAX_HW_QUEUES to the host (HIP's
  * default is 4; the Python package and bench.py raise it to 32 before HIP initialises, see
- * INTEGRATION.md). */
+ * INTEGRATION.md) and only reads it: with auto in-flight, a deferred loop spreads its ~16
+ * overlapping frames over at most half the queues — slots tracing launch groups of several
+ * consecutive frames each (16 x 1 with 32 queues, 2 x 8 with HIP's default 4). */
 #define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
 #define TRT_FRAMES_IN_FLIGHT_AUTO 0u
 /* Fixed by the ABI (a host cannot change it): the upper bound of n.  The library's own slot
@@ -171,8 +173,9 @@ int trt_set_frames_in_flight(trt_ctx* ctx, uint32_t n);
  * k of the launch owns blocks [k * ntiles, (k + 1) * ntiles), so a frame's slowest tiles overlap
  * the next frame's tiles inside one grid and the GPU drains once per launch instead of once per
  * frame.  n in [1, TRT_MAX_FRAME_BATCH]: 1 = one launch per frame (the reference's dispatch per
- * frame); 0 = auto (the default): up to TRT_MAX_FRAME_BATCH frames per launch.  Split and
- * deferred-shadow frames always launch one frame at a time (per-frame scratch). */
+ * frame); 0 = auto (the default): up to TRT_MAX_FRAME_BATCH frames per launch.  Split frames
+ * launch one frame at a time; deferred-shadow frames in launch groups of their own (above),
+ * each frame of a group with its own scratch. */
 #define TRT_FRAME_BATCH_AUTO 0u
 #define TRT_MAX_FRAME_BATCH 64u
 int trt_set_frame_batch(trt_ctx* ctx, uint32_t n);

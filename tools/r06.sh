@@ -79,6 +79,18 @@ for stage in "$@"; do
         tests/golden/dropin_meshes.bin 192 "$2" >> "$OUT/groups_cabi.log" 2>&1 || exit 1
     done
     grep bench "$OUT/groups_cabi.log" ;;
+  pmc) # PMC passes (one counter group per rocprofv3 run) over PMC_CMD, summarised per kernel
+    CMD=${PMC_CMD:-python3 tools/kbench.py --config ref --frames 48 --inflight 16}
+    i=0
+    IFS=';' read -ra sets <<< "${PMC_SETS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE;TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE}"
+    for set_ in "${sets[@]}"; do
+      i=$((i + 1))
+      (export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $set_ --kernel-trace --output-format csv \
+        -d "$OUT/pmc/p$i" -o run -- $CMD > "$OUT/pmc_p$i.log" 2>&1) || { echo "pmc pass $i failed"; tail -5 "$OUT/pmc_p$i.log"; exit 1; }
+    done
+    python tools/pmc_kernels.py "$OUT/pmc" > "$OUT/pmc_kernels.jsonl"
+    find "$OUT/pmc" -name '*kernel_trace.csv' -delete
+    cut -c1-400 "$OUT/pmc_kernels.jsonl" | head -8 ;;
   cabi) # the shipped frame through the C++ host: HIP's default queues (auto / 4 in flight), 32 queues
     for cf in "unset 0" "unset 4" "unset 2" "32 0"; do
       set -- $cf
