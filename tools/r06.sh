@@ -62,6 +62,19 @@ for stage in "$@"; do
       done
     done
     python tools/ab_summary.py "$OUT/ab.jsonl" ;;
+  envab) # interleaved A/B of runtime knobs: AB_ENVS="name:VAR=val,VAR=val name2:VAR=val", AB_LEGS as ab
+    IFS=';' read -ra legs <<< "${AB_LEGS:-C2|--frames 200 --frame-batch 1 --inflight 2}"
+    for round in $(seq 1 "${AB_ROUNDS:-2}"); do
+      for spec in ${AB_ENVS:-cur:}; do
+        name=${spec%%:*}; kv=${spec#*:}
+        for leg in "${legs[@]}"; do
+          cfg=${leg%%|*}; args=${leg#*|}
+          env ${kv//,/ } timeout -k 10 300 python tools/kbench.py --config "$cfg" $args --tag "$name:$cfg:$args" \
+            >> "$OUT/envab.jsonl" 2>> "$OUT/envab.err" || { tail -5 "$OUT/envab.err"; exit 1; }
+        done
+      done
+    done
+    python tools/ab_summary.py "$OUT/envab.jsonl" ;;
   groups) # deferred frame groups (TRT_DEFER_GROUP = G frames per launch, N groups in flight)
     for round in 1 2; do
       for gn in "1 16" "2 8" "4 4" "8 2" "16 1"; do
