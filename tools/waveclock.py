@@ -21,8 +21,6 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--out", default="")
-    ap.add_argument("--halves", action="store_true",
-                    help="two-wave tiles (trace_halves): also the per-wave walk times and SIMD placement")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -41,10 +39,9 @@ def main():
     for _ in range(a.frames):
         r.draw_frame(p, out8=out8, out32=rec)
         torch.cuda.synchronize()
-        allr = rec.view(torch.int32).flatten()[: 8 * ntiles].cpu().numpy().view(np.uint32)
-        res.append(allr.copy())
-    raw = res[-1][: 4 * ntiles].reshape(ntiles, 4)
-    extra = res[-1][4 * ntiles:].reshape(ntiles, 4)
+        raw = rec.view(torch.int32).flatten()[: 4 * ntiles].cpu().numpy().view(np.uint32).reshape(ntiles, 4)
+        res.append(raw.copy())
+    raw = res[-1]
     t0 = (raw[:, 3].astype(np.int64) << 32) | raw[:, 1].astype(np.int64)
     t1 = t0 + raw[:, 2].astype(np.int64)
     xcd = raw[:, 0] >> 28
@@ -74,17 +71,6 @@ def main():
         "last_start_us": float(s.max()) / 1e3,
         "per_xcd_busy_end_us": [float(e[xcd == k].max()) / 1e3 for k in range(8) if (xcd == k).any()],
     }
-    if a.halves:
-        own, hlp = extra[:, 0].astype(np.int64) * 10, extra[:, 2].astype(np.int64) * 10  # ns
-        hw0, hw1 = extra[:, 1], extra[:, 3]
-        simd = lambda h: (h >> 4) & 3
-        cu = lambda h: (h >> 8) & 15
-        out["owner_walk_us"] = {q: float(np.percentile(own, q)) / 1e3 for q in (50, 90, 99, 100)}
-        out["helper_walk_us"] = {q: float(np.percentile(hlp, q)) / 1e3 for q in (50, 90, 99, 100)}
-        top = np.argsort(dur)[-64:]
-        out["slowest64_owner_helper_us"] = [float(own[top].mean()) / 1e3, float(hlp[top].mean()) / 1e3]
-        out["same_simd_frac"] = float(((simd(hw0) == simd(hw1)) & (cu(hw0) == cu(hw1))).mean())
-        out["same_cu_frac"] = float((cu(hw0) == cu(hw1)).mean())
     print(json.dumps(out), flush=True)
     if a.out:
         np.savez_compressed(a.out, raw=raw, tile=tile, xcd=xcd, start_ns=s, end_ns=e, width=p.width)

@@ -80,7 +80,6 @@ struct trt_ctx {
     uint32_t defer_sub = 0;
     uint32_t cur_in_flight = 1; // frames in flight of the current render call
     bool spp_lanes = true;      // spp > 1 frames: one lane per sample (TRT_SPP_LANES)
-    uint32_t tile_halves = 0;   // triangle-free single-frame launches: two waves per tile split at this spine depth (TRT_TILE_HALVES, 0 = off)
     // Subtree-split scratch, one set per frames-in-flight slot (concurrent frames must not share
     // task queues): two task queues, per-pixel fixed-point colours, the split-pixel list and
     // the counters.

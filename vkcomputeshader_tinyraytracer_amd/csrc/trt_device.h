@@ -252,7 +252,6 @@ struct KArgs {
     uint32_t px_fstride;
     size_t ev_fstride, shq_fstride;
     uint32_t spp_lanes;               // spp > 1: one lane per sample (trace_samples), spp waves per tile
-    uint32_t tile_halves;             // triangle-free single-frame launches: two waves per tile (trace_halves)
     FrameRec fr[kMaxLaunchFrames];    // camera + output of each frame of the launch
 };
 static_assert(sizeof(KArgs) <= 4096, "KArgs fits the 4 KB kernel-argument limit");

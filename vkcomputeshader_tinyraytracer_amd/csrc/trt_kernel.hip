@@ -1589,39 +1589,15 @@ __device__ __forceinline__ MatVals load_mat(const KArgs& A, int kind, int idx, f
 // HYB: the deferred refraction children live in CAP LDS entries plus a private tail.  (The
 // shading here is written out rather than through resolve_hit / light_term / make_children:
 // the factored form compiles the C2 and C4 kernels with more live registers — C2 spilled.)
-// HALF (trace_halves, triangle-free single-frame launches).  The pixel's "spine" is the chain of
-// last-popped children from the root (the refraction child where there is one, else the
-// reflection child): a segment is on it exactly when the stack is empty as it is taken, and the
-// subtree of the spine segment at depth S (A.tile_halves) is the tail of the pixel's pop order.
-// 1 = the owner wave: everything but that subtree (the spine segment at depth S - 1 drops its
-// last child); 2 = the helper wave: the spine down to depth S intersected but not shaded (no
-// colour term, no shadow rays, only the last child followed), then that subtree with its colour
-// terms recorded to `terms` ([term][component] rows of 64 lanes, this lane's column) in pop
-// order; it returns their count in .x.
-template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool HYB = SPLIT, int HALF = 0>
+template <int CAP, bool COUNT, int GEOM, bool SPLIT, bool HYB = SPLIT>
 __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float* lds, float4* slab,
-                                       uint32_t pixel, bool& spilled, float* terms = nullptr) {
-    static_assert(HALF == 0 || (GEOM == 0 && !SPLIT && !HYB && !COUNT), "tile halves: triangle-free plain frames");
+                                       uint32_t pixel, bool& spilled) {
     const int D = (int)A.max_depth;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    uint32_t nterm = 0;
-    auto emit = [&](f3 term) { // the running sum of shader.comp:458 / 507, or the helper's record
-        if constexpr (HALF == 2) {
-            terms[(nterm * 3u + 0u) * 64u] = term.x;
-            terms[(nterm * 3u + 1u) * 64u] = term.y;
-            terms[(nterm * 3u + 2u) * 64u] = term.z;
-            ++nterm;
-        } else {
-            color = add(color, term);
-        }
-    };
     using Stk = typename StackOf<CAP, HYB, GEOM>::type;
     typename Stk::Mem stk_mem;
     Stk stk(lds, stk_mem);
-    const int S = HALF ? (int)A.tile_halves : 0;
     for (;;) {
-        // the helper's spine above depth S: its last child only
-        const bool skip_root = HALF == 2 && stk.n == 0 && cur.depth < S;
         if (COUNT && cur.depth > 0) ++cnt.sec;
 #ifdef TRT_DIAG_PIXEL_WORK
         ++cnt.wseg;
@@ -1632,10 +1608,8 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
         Seg next;
         if (h.kind == HIT_NONE) {
             if (COUNT) ++cnt.miss;
-            if (!skip_root) {
-                f3 bg = background(A, cur.d);
-                emit(muls(bg, cur.thr));
-            }
+            f3 bg = background(A, cur.d);
+            color = add(color, muls(bg, cur.thr));
         } else {
             // Resolve the closest hit: point, normal, material (shader.comp:302-360).
             f3 p = add(cur.o, muls(cur.d, h.t));
@@ -1757,7 +1731,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
 #define TRT_LIGHT_UNROLL 0
 #endif
             constexpr int kLightUnroll = GEOM >= 2 && !TRT_LIGHT_UNROLL ? 1 : 3;
-            if (!skip_root)
 #pragma unroll kLightUnroll
             for (int i = 0; i < 3; ++i) {
                 f3 L = mk(A.light[i][0], A.light[i][1], A.light[i][2]);
@@ -1803,7 +1776,7 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 specular = add(specular, muls(kdv, spec));
             }
             } // !LATE
-            if (!skip_root) emit(muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
+            color = add(color, muls(add(muls(diffuse, alb[0]), muls(specular, alb[1])), cur.thr));
             // Children (shader.comp:509-575).  Children that the reference would push and
             // then drop unseen at the depth / throughput test (shader.comp:449) are not made.
             const int cd = cur.depth + 1;
@@ -1839,11 +1812,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
                 if (sb) mk_refr = false;
                 spilled = spilled || sa || sb;
             }
-            if (HALF == 1 && stk.n == 0 && cur.depth == S - 1) { // the helper wave traces the last child
-                if (mk_refr) mk_refr = false;
-                else mk_refl = false;
-            }
-            if (skip_root && mk_refr) mk_refl = false; // the owner wave traces the other child
             // Reference pushes refraction then reflection and pops reflection first.
             if (mk_refl) {
                 if (mk_refr) stk.push(refr);
@@ -1862,7 +1830,6 @@ __device__ __forceinline__ f3 cast_seg(const KArgs& A, Seg cur, Cnt& cnt, float*
             break;
         }
     }
-    if constexpr (HALF == 2) return mk((float)nterm, 0.0f, 0.0f);
     return color;
 }
 
@@ -2542,82 +2509,6 @@ __global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void 
     if (COUNT) flush_counts(A, cnt);
 }
 
-// ---- single-frame launches of triangle-free frames: two waves per tile (KArgs::tile_halves) ----
-//
-// A single-frame launch (the reference's drawFrame pacing: one dispatch per frame, main.cpp:2181-
-// 2205) lasts as long as its slowest tile, and in a C2 frame that is a glass tile whose pixels
-// each walk a tree of up to 2^D - 1 segments one after the other, every miss a dependent envmap
-// gather (31 us launch, its longest tile 26 us: profiles/r05t_clock_c2_single_frame.log).  Here
-// a tile is a 128-lane workgroup: wave 1 (the helper) follows each pixel's spine (cast_seg HALF)
-// to depth S without shading it and traces the subtree there, recording its colour terms in LDS
-// in order; wave 0 (the owner) traces the rest of the tree.  The reference pushes the
-// refraction child first and pops the reflection child first (shader.comp:559-575), so that
-// subtree is the tail of the pixel's pop order: the owner adds the helper's terms after its own
-// with the same additions — bit-identical to cast_seg's loop.  The subtree spans depths
-// S .. D - 1, at most 2^(D-S) - 1 <= 2^CAP - 1 segments, so the record never overflows.
-template <int CAP>
-__global__ __launch_bounds__(128, TRT_G0_WAVES) void trace_halves(KArgs A) {
-    static_assert(CAP >= 1 && CAP <= LDS_STACK_MAX && seg_lds<CAP, 0>(), "LDS segment stacks");
-    constexpr int K = (1 << CAP) - 1;
-    constexpr int SF = lds_stack_floats<CAP, 0>();
-    __shared__ float lds[2 * SF];        // the two waves' segment stacks
-    __shared__ float terms[K * 3 * 64 + 64]; // the helper's terms [term][component][lane], its counts
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6u), lane = threadIdx.x & 63u;
-#ifdef TRT_DIAG_WAVE_CLOCK
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    const uint32_t tile = xcd_tile(A, blockIdx.x);
-    const FrameRec& F = A.fr[0];
-    const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u), k = (tile / A.ntx) * 8u + (lane >> 3);
-    const bool valid = tile < A.ntiles && x < A.width && k < A.rows;
-    Cnt cnt;
-    bool unused = false;
-    f3 c = mk(0.0f, 0.0f, 0.0f);
-    if (valid) {
-        const Seg root{mk(F.cam[0], F.cam[1], F.cam[2]), primary_dir(A, x, band_row(A, k), 0), 1.0f, 0};
-        // DeferStack addresses lds + threadIdx.x: wave 1's columns start at lds + SF
-        if (w == 0u) c = cast_seg<CAP, false, 0, false, false, 1>(A, root, cnt, lds, nullptr, 0u, unused);
-        else c = cast_seg<CAP, false, 0, false, false, 2>(A, root, cnt, lds + SF - 64, nullptr, 0u, unused, terms + lane);
-    }
-    if (w == 1u) terms[K * 3 * 64 + lane] = valid ? c.x : 0.0f;
-#ifdef TRT_DIAG_WAVE_CLOCK
-    // diagnostic: waveclock.py's record per workgroup in out32, then per wave (duration to the
-    // end of its walk, HW_ID) at out32 + 4 * ntiles
-    {
-        const uint64_t t_walk = __builtin_amdgcn_s_memrealtime();
-        uint32_t hwid, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        uint32_t* rec = reinterpret_cast<uint32_t*>(A.out32);
-        if (lane == 0u && rec) {
-            rec[4 * (A.ntiles + blockIdx.x) + 2u * w] = (uint32_t)(t_walk - t_start);
-            rec[4 * (A.ntiles + blockIdx.x) + 2u * w + 1u] = hwid;
-            if (w == 0u) {
-                rec[4 * blockIdx.x] = tile | ((xcc & 15u) << 28);
-                rec[4 * blockIdx.x + 1] = (uint32_t)t_start;
-                rec[4 * blockIdx.x + 3] = (uint32_t)(t_start >> 32);
-            }
-        }
-    }
-#endif
-    __syncthreads();
-    if (w != 0u || !valid) {
-#ifdef TRT_DIAG_WAVE_CLOCK
-        if (w == 0u && lane == 0u && A.out32)
-            reinterpret_cast<uint32_t*>(A.out32)[4 * blockIdx.x + 2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-#endif
-        return;
-    }
-    const uint32_t n = (uint32_t)terms[K * 3 * 64 + lane];
-    for (uint32_t i = 0; i < n; ++i)
-        c = add(c, mk(terms[(i * 3u + 0u) * 64u + lane], terms[(i * 3u + 1u) * 64u + lane], terms[(i * 3u + 2u) * 64u + lane]));
-    store_pixel(A, F, (size_t)k * A.width + x, mk(clamp01(c.x), clamp01(c.y), clamp01(c.z))); // shader.comp:582
-#ifdef TRT_DIAG_WAVE_CLOCK
-    if (lane == 0u && A.out32)
-        reinterpret_cast<uint32_t*>(A.out32)[4 * blockIdx.x + 2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-#endif
-}
-
 // One round of a split frame: persistent waves take 64 tasks at a time (static schedule) from
 // the previous launch's queue, trace each task's subtree within the depth window (its
 // window-edge children go to the next queue) and add the subtree's colour to its pixel's
@@ -2964,14 +2855,6 @@ hipError_t launch_trace(const KArgs& A, hipStream_t stream, bool count) {
         }
 #undef TRT_SPLIT
 #undef TRT_SPLIT_G
-        return hipGetLastError();
-    }
-    if (A.tile_halves && A.tile_halves < D && geom == 0 && !count && A.nframes <= 1u && A.spp <= 1u && D >= 2u && D <= 4u) {
-        // triangle-free single-frame launches: two waves per tile (trace_halves; at D = 5 the
-        // 15-term record and two 4-entry stacks would cost the 5-wave occupancy)
-        if (D == 2u) hipLaunchKernelGGL((trace_halves<1>), grid, dim3(128), 0, stream, A);
-        else if (D == 3u) hipLaunchKernelGGL((trace_halves<2>), grid, dim3(128), 0, stream, A);
-        else hipLaunchKernelGGL((trace_halves<3>), grid, dim3(128), 0, stream, A);
         return hipGetLastError();
     }
     // a plain launch traces A.nframes frames: ntiles blocks per frame (frame-major)

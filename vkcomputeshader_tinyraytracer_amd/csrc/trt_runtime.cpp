@@ -224,7 +224,6 @@ int trt_create(trt_ctx** out, int hip_device) {
     }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
     if (const char* e = std::getenv("TRT_SPP_LANES")) c->spp_lanes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("TRT_TILE_HALVES")) c->tile_halves = (uint32_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32 or 16
         const int ppw = std::atoi(e);
         c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
@@ -607,10 +606,6 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // spp a power of two in [2, 64] and no replayed rays: one lane per sample (trace_samples;
     // TRT_SPP_LANES=0 keeps the per-pixel sample loop)
     A.spp_lanes = (A.spp >= 2u && A.spp <= 64u && (A.spp & (A.spp - 1u)) == 0u && !p->rays_in && c->spp_lanes) ? 1u : 0u;
-    // triangle-free single-frame launches (max_depth 2..4): two waves per tile, the second
-    // tracing the subtree of the spine segment at depth tile_halves (trace_halves;
-    // TRT_TILE_HALVES=0 keeps one wave)
-    A.tile_halves = c->tile_halves;
     A.seed = p->seed;
     A.flags = p->flags;
     // dir_z = -1.0 * (HEIGHT / (2.0 * tan(fov / 2.0))) in double, main.cpp:1503
