@@ -273,23 +273,28 @@ def test_auto_in_flight_drops_a_slot_that_runs_out_of_memory(scenes, monkeypatch
         r.close()
 
 
-@pytest.mark.parametrize("group,inflight", [(2, 0), (3, 2), (4, 4), (8, 1), (16, 0)])
-def test_deferred_frame_groups(scenes, group, inflight):
+@pytest.mark.parametrize("group,inflight,inter", [(2, 0, 2), (3, 2, 2), (4, 4, 2), (8, 1, 2), (16, 0, 2),
+                                                 (3, 2, 0), (8, 1, 0), (3, 2, 1), (8, 1, 1)])
+def test_deferred_frame_groups(scenes, group, inflight, inter):
     """TRT_DEFER_GROUP: consecutive deferred frames of a frame loop traced by one launch sequence
     (pass A over every frame's tiles, one pass B and one pass C over all of them, each frame with
-    its own scratch).  Ragged groups (the loop's last group is shorter), groups in flight and
-    both scenes: every frame equals the single deferred frame of its UBO bit for bit."""
+    its own scratch), their blocks dealt frame-major (TRT_DEFER_INTER=0), interleaved frame by
+    frame in pass A (1) or in all three passes (2, the default).  Ragged groups (the loop's last
+    group is shorter), groups in flight and both scenes: every frame equals the single deferred
+    frame of its UBO bit for bit."""
     import vkcomputeshader_tinyraytracer_amd as trt
 
-    old = os.environ.get("TRT_DEFER_GROUP")
-    os.environ["TRT_DEFER_GROUP"] = str(group)
+    knobs = {"TRT_DEFER_GROUP": str(group), "TRT_DEFER_INTER": str(inter)}
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
     try:
         r = trt.Renderer(0)
     finally:
-        if old is None:
-            os.environ.pop("TRT_DEFER_GROUP", None)
-        else:
-            os.environ["TRT_DEFER_GROUP"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         for name in ("ref", "readme"):
             sc = scenes[name]

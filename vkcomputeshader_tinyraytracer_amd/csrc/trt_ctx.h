@@ -69,6 +69,7 @@ struct trt_ctx {
     uint32_t defer_in_flight = 16; // auto frames in flight of deferred-shadow loops (TRT_DEFER_IN_FLIGHT env)
     // frames per deferred launch group of a frame loop: TRT_DEFER_GROUP env, 0 = auto (by the
     // hardware queues: render_frame_list)
+    uint32_t defer_inter = 2;   // TRT_DEFER_INTER: a frame group's blocks dealt frame by frame: 0 = off, 1 = pass A, 2 = passes A, B, C
     uint32_t defer_group = 0;
     // hardware queues HIP gives this process: GPU_MAX_HW_QUEUES at trt_create (HIP's default 4
     // when unset); the library only reads it

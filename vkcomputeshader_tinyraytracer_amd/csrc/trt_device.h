@@ -249,6 +249,7 @@ struct KArgs {
     // frames of a deferred launch (trt_render_frames groups consecutive frames): frame f's
     // scratch is ev + f * ev_fstride, shq + f * shq_fstride, px_ev / fb + f * px_fstride, dctr + f
     uint32_t dframes;
+    uint32_t defer_inter;             // a group's blocks frame by frame: 1 = pass A (trace_kernel), 2 = passes A, B, C
     uint32_t px_fstride;
     size_t ev_fstride, shq_fstride;
     uint32_t spp_lanes;               // spp > 1: one lane per sample (trace_samples), spp waves per tile

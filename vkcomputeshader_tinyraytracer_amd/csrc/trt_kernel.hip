@@ -2481,8 +2481,13 @@ __global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void 
         }
     } else if (DEFER && !SPLIT) { // defer_sub waves per tile of each of dframes frames (trace_tile)
         const uint32_t Sd = A.defer_sub > 1u ? A.defer_sub : 1u, per = A.ntiles * Sd;
-        f = vb / per;
-        t = vb - f * per;
+        if (A.defer_inter && A.dframes > 1u) { // the group's frames block by block: they advance together
+            f = vb % A.dframes;
+            t = vb / A.dframes;
+        } else {
+            f = vb / per;
+            t = vb - f * per;
+        }
         tile = xcd_tile(A, t / Sd);
         trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % Sd, f);
         return;
@@ -2610,7 +2615,9 @@ template <int GEOM>
 __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArgs A) {
     __shared__ float4 slab[slab_float4s<GEOM>()];
     Cnt cnt;
-    const uint32_t per = gridDim.x / max(A.dframes, 1u), f = blockIdx.x / per, b = blockIdx.x - f * per;
+    const uint32_t F = max(A.dframes, 1u), per = gridDim.x / F;
+    const bool inter = A.defer_inter > 1u && F > 1u; // frames block by block (pass A's dealing)
+    const uint32_t f = inter ? blockIdx.x % F : blockIdx.x / per, b = inter ? blockIdx.x / F : blockIdx.x - f * per;
     const DScratch S = dscratch(A, f);
     const uint32_t s = b % kDeferStripes, K = per / kDeferStripes;
     const uint32_t n = min(S.dctr->nq[s * kCtrStride], A.shq_cap);
@@ -2633,7 +2640,10 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArg
 // colour += thr * (diffuse * albedo.x + specular * albedo.y)); then clamp, gamma and the dual
 // store.  Lane = the pixel's lane in its pass-A tile; block f * ntiles + tile: frame f.
 __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
-    const uint32_t f = blockIdx.x / A.ntiles, tile = blockIdx.x - f * A.ntiles, lane = threadIdx.x;
+    const uint32_t F = max(A.dframes, 1u);
+    const bool inter = A.defer_inter > 1u && F > 1u; // frames block by block (pass A's dealing)
+    const uint32_t f = inter ? blockIdx.x % F : blockIdx.x / A.ntiles;
+    const uint32_t tile = inter ? blockIdx.x / F : blockIdx.x - f * A.ntiles, lane = threadIdx.x;
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;

@@ -229,6 +229,7 @@ int trt_create(trt_ctx** out, int hip_device) {
         c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
     }
     if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) c->hw_queues = (uint32_t)std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("TRT_DEFER_INTER")) c->defer_inter = (uint32_t)std::min(2, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_DEFER_GROUP"))
         c->defer_group = (uint32_t)std::min((int)trt::kMaxLaunchFrames, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT"))
@@ -841,6 +842,7 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
     // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
     A.defer_sub = c->defer_sub ? c->defer_sub : (c->cur_in_flight * G <= 4u ? 2u : 1u);
+    A.defer_inter = c->defer_inter;
     // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
     A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", z.chunks / trt::kDeferStripes);
     A.shq_cap = (uint32_t)env_cap("TRT_DEFER_QCAP", z.qcap / trt::kDeferStripes);
