@@ -3,7 +3,7 @@
 # entries interleaved per round to cancel drift.  An entry is a variant name
 # (variants/libtrt_<name>.so) or "prod" (the in-tree build), optionally followed by
 # "+VAR=value" environment settings:
-#   LIBS="prod prod+TRT_BVH_COMPRESS=0 unode" CFGS="C4 C3 ref" ROUNDS=2 FRAMES=20 tools/ab_libs.sh
+#   LIBS="prod prod+TRT_DEFER_INTER=0 sh4" CFGS="C4 C3 ref" ROUNDS=2 FRAMES=20 tools/ab_libs.sh
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 for r in $(seq 1 "${ROUNDS:-2}"); do
   for cfg in ${CFGS:-C4 C3 ref readme}; do

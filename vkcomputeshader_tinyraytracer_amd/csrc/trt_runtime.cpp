@@ -134,9 +134,6 @@ Mat to_mat(const trt_material& m) {
     return r;
 }
 
-// TRT_BVH_COMPRESS: 0 = no 48-B nodes (default: measured slower), 1 = for
-// the 4-wave BVH build, 2 = every BVH4 walk; the kernel walks them only when built with
-// -DTRT_BVH_COMPRESS=1.  Read at every scene upload / frame.
 void fill_ubo_args(KArgs& A, const trt_ubo& u) {
     const trt_sphere* s[4] = {&u.sphere0, &u.sphere1, &u.sphere2, &u.sphere3};
     for (int i = 0; i < 4; ++i) {
@@ -661,7 +658,6 @@ void fill_args(trt_ctx* c, const trt_params* p, KArgs& A) {
     // vary more from frame to frame and a pair doubles the longest wave),
     // profiles/r03_ab_frame_pair.log
     A.frame_group = c->frame_group > 0 ? (uint32_t)c->frame_group : (c->nbatch == 0 ? 2u : 1u);
-    // 48-B nodes (TRT_BVH_COMPRESS, opt-in; 0 = off is the default): for the 4-wave build (mode 1) or for every BVH4 walk (mode 2)
 }
 
 // Does this frame run deferred shadows?  Auto: mesh scenes with max_depth >= 8, whose deep
