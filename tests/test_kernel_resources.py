@@ -40,9 +40,11 @@ def test_c2_kernel_has_no_scratch(resources):
 
 def test_c4_kernel_scratch_budget(resources):
     """C4 (depth 4, quantized BVH4): 96 VGPRs, the private segment stack (96 B) and the
-    traversal stack tail (192 B) plus the measured spill slots (432 B in round 5)."""
+    traversal stack tail (192 B) plus the measured spill slots: 432 B in rounds 5 and 6, the
+    budget exactly (a build that spills more fails; the spill-free 4-wave build is 9 % slower,
+    DESIGN §7)."""
     r = resources["3, false, 3, false, false, false"]
-    assert r["vgpr"] <= 96 and r["scratch"] <= 448, r
+    assert r["vgpr"] <= 96 and r["scratch"] <= 432, r
 
 
 def test_lds_fits_the_wave_targets(resources):
