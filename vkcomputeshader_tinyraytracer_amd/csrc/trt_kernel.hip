@@ -2481,9 +2481,22 @@ __global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void 
         }
     } else if (DEFER && !SPLIT) { // defer_sub waves per tile of each of dframes frames (trace_tile)
         const uint32_t Sd = A.defer_sub > 1u ? A.defer_sub : 1u, per = A.ntiles * Sd;
-        if (A.defer_inter && A.dframes > 1u) { // the group's frames block by block: they advance together
-            f = vb % A.dframes;
-            t = vb / A.dframes;
+        if (A.defer_inter && A.dframes > 1u) {
+            // the group's frames block by block, so they advance together; within each XCD
+            // (block vb runs on XCD vb % 8), so every XCD traces every frame, with frame f's
+            // chunk classes (xcd_tile: class t % 8) rotated by f as inter_tile does, so every
+            // XCD also sees every class (a costly class on one XCD would end the group late);
+            // blocks past the last whole round of 8 are dealt frame by frame
+            const uint32_t F = A.dframes, per8 = per & ~7u;
+            if (vb < F * per8) {
+                const uint32_t x = vb & 7u, j = vb >> 3;
+                f = j % F;
+                t = (j / F) * 8u + ((x + f) & 7u);
+            } else {
+                const uint32_t r = vb - F * per8, nl = per - per8;
+                f = r / nl;
+                t = per8 + r % nl;
+            }
         } else {
             f = vb / per;
             t = vb - f * per;
@@ -2640,10 +2653,27 @@ __global__ __launch_bounds__(64, waves_per_simd<GEOM>()) void defer_shadows(KArg
 // colour += thr * (diffuse * albedo.x + specular * albedo.y)); then clamp, gamma and the dual
 // store.  Lane = the pixel's lane in its pass-A tile; block f * ntiles + tile: frame f.
 __global__ __launch_bounds__(64) void defer_resolve(KArgs A) {
-    const uint32_t F = max(A.dframes, 1u);
-    const bool inter = A.defer_inter > 1u && F > 1u; // frames block by block (pass A's dealing)
-    const uint32_t f = inter ? blockIdx.x % F : blockIdx.x / A.ntiles;
-    const uint32_t tile = inter ? blockIdx.x / F : blockIdx.x - f * A.ntiles, lane = threadIdx.x;
+    const uint32_t F = max(A.dframes, 1u), lane = threadIdx.x;
+    uint32_t f, tile;
+    if (A.defer_inter > 1u && F > 1u) {
+        // pass A's dealing (trace_kernel): tile t of frame f on the XCD whose pass-A block traced
+        // it (one pass-A wave per tile when a group runs), so its events are in that XCD's L2
+        const uint32_t vb = blockIdx.x, per8 = A.ntiles & ~7u;
+        uint32_t t;
+        if (vb < F * per8) {
+            const uint32_t j = vb >> 3;
+            f = j % F;
+            t = (j / F) * 8u + (((vb & 7u) + f) & 7u);
+        } else {
+            const uint32_t r = vb - F * per8, nl = A.ntiles - per8;
+            f = r / nl;
+            t = per8 + r % nl;
+        }
+        tile = xcd_tile(A, t);
+    } else {
+        f = blockIdx.x / A.ntiles;
+        tile = blockIdx.x - f * A.ntiles;
+    }
     const uint32_t x = (tile % A.ntx) * 8u + (lane & 7u);
     const uint32_t k = (tile / A.ntx) * 8u + (lane >> 3);
     if (x >= A.width || k >= A.rows) return;
