@@ -504,7 +504,7 @@ def extra_frame(dev: int, name: str, frames: int, args) -> dict:
         ms2 = r2["elapsed"] / frames * 1e3
         out["at_2_in_flight"] = {
             "note": "MAX_FRAMES_IN_FLIGHT = 2 (main.cpp:45), the reference's pacing; the leg above runs the "
-                    "library's auto count (16 for deferred-shadow frames)",
+                    "library's auto shape (deferred-shadow frames: 8 slots x 3-frame groups with 32 hardware queues)",
             "ms_per_frame": round(ms2, 4), "fps": round(1e3 / ms2, 2),
             "mray_s": round(r2["rays_total"] / r2["elapsed"] / 1e6, 3),
             "latency_ms": round(r2["kernel_ms_per_frame"], 4),

@@ -155,9 +155,9 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * the README scene -28 %, profiles/r04z_ab_deferred_in_flight.jsonl).  Each slot is a HIP stream, so the process
  * needs as many hardware queues: the library leaves GPU_MAX_HW_QUEUES to the host (HIP's
  * default is 4; the Python package and bench.py raise it to 32 before HIP initialises, see
- * INTEGRATION.md) and only reads it: with auto in-flight, a deferred loop spreads its ~16
- * overlapping frames over at most half the queues — slots tracing launch groups of several
- * consecutive frames each (16 x 1 with 32 queues, 2 x 8 with HIP's default 4). */
+ * INTEGRATION.md) and only reads it: with auto in-flight, a deferred loop runs slots tracing
+ * launch groups of several consecutive frames each, on at most half the queues: 8 slots x 3
+ * frames with >= 16 queues, 2 x 8 with HIP's default 4. */
 #define TRT_FRAMES_IN_FLIGHT_DEFAULT 0u
 #define TRT_FRAMES_IN_FLIGHT_AUTO 0u
 /* Fixed by the ABI (a host cannot change it): the upper bound of n.  The library's own slot

@@ -258,11 +258,12 @@ def test_auto_in_flight_drops_a_slot_that_runs_out_of_memory(scenes, monkeypatch
         monkeypatch.setenv("TRT_ENABLE_TEST_HOOKS", "1")
         monkeypatch.setenv("TRT_TEST_FAIL_DEFER_SLOT", "2")
         p = sc.params()
-        out = torch.zeros((6, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
+        n = 24  # enough frames to reach slot 2 with any automatic shape (8 slots x 3 at >= 16 queues)
+        out = torch.zeros((n, p.height, p.width, 4), dtype=torch.uint8, device="cuda")
         r.set_deferred_shadows(DEFER_ON)
-        r.render_frames(p, out, 6, frame_stride=p.height * p.width * 4)
+        r.render_frames(p, out, n, frame_stride=p.height * p.width * 4)
         torch.cuda.synchronize()
-        for f in range(6):
+        for f in range(n):
             assert np.array_equal(out[f].cpu().numpy(), u8), f
         # an explicit in-flight count is the caller's: the same failure is reported, not hidden
         r.set_frames_in_flight(4)

@@ -67,6 +67,7 @@ struct trt_ctx {
     int frame_group = -1; // TRT_FRAME_GROUP (1 or 2); -1 = auto: 2 for triangle-free scenes, else 1
     int bvh_waves4 = -1; // TRT_BVH_WAVES4 env: 0 / 1 forces the BVH build, -1 = by scene size
     uint32_t defer_in_flight = 16; // auto frames in flight of deferred-shadow loops (TRT_DEFER_IN_FLIGHT env)
+    bool defer_in_flight_set = false; // TRT_DEFER_IN_FLIGHT given: it shapes the loop at every queue count (defer_shape)
     // frames per deferred launch group of a frame loop: TRT_DEFER_GROUP env, 0 = auto (by the
     // hardware queues: render_frame_list)
     uint32_t defer_inter = 2;   // TRT_DEFER_INTER: a frame group's blocks dealt frame by frame: 0 = off, 1 = pass A, 2 = passes A, B, C

@@ -229,8 +229,10 @@ int trt_create(trt_ctx** out, int hip_device) {
     if (const char* e = std::getenv("TRT_DEFER_INTER")) c->defer_inter = (uint32_t)std::min(2, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_DEFER_GROUP"))
         c->defer_group = (uint32_t)std::min((int)trt::kMaxLaunchFrames, std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT"))
+    if (const char* e = std::getenv("TRT_DEFER_IN_FLIGHT")) {
         c->defer_in_flight = (uint32_t)std::min((int)TRT_BUILD_MAX_IN_FLIGHT, std::max(1, std::atoi(e)));
+        c->defer_in_flight_set = true;
+    }
     if (const char* e = std::getenv("TRT_XCD_ROT")) c->xcd_rot = (uint32_t)std::min(8, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_SKEW")) c->xcd_skew = (uint32_t)std::min(7, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("TRT_XCD_INTER")) c->xcd_inter = (uint32_t)std::min(2, std::max(0, std::atoi(e)));
@@ -744,12 +746,14 @@ bool defer_bufs_fit(const trt_ctx::SplitBufs& b, const DeferSizes& z, size_t npx
 
 // Deferred frame loop shape: `group` frames per launch sequence on each of `slots` in-flight
 // slots.  Explicit: TRT_DEFER_GROUP, or trt_set_frames_in_flight (then groups of 1, the
-// reference's pacing when it is 2).  Auto: about defer_in_flight (16) frames overlap in all,
-// spread over at most half the process's hardware queues — a stream per slot, and slots sharing
-// a queue serialise: with 32 queues 16 slots of 1 frame; with HIP's default 4 queues 2 slots of
-// 8 frames (the shipped frame through the C++ host 0.82 -> 0.55 ms per frame;
-// profiles/r06f_defer_groups_cabi_default_queues.log; at 32 queues groups of 2 / 4 / 8 tie / lose
-// 14 % / 25 %, profiles/r06f_ab_defer_groups.jsonl).
+// reference's pacing when it is 2).  Auto, with the group's frames dealt block by block
+// (defer_inter): with at least 16 hardware queues 8 slots of 3 frames (24 in flight: the shipped
+// frame 320 -> 311 us, the README scene 155 -> 149 us against 16 slots of 1, at half the frame
+// latency; profiles/r06t_ab_defer_shape_32q.jsonl); with fewer, defer_in_flight (16) frames over
+// at most half the queues — a stream per slot, and slots sharing a queue serialise: with HIP's
+// default 4 queues 2 slots of 8 frames (the shipped frame through the C++ host 0.82 -> 0.51 ms
+// per frame; 2 x 12 and 6 x 4 within 2 %, profiles/r06t_shape_q4.log).  An explicit
+// TRT_DEFER_IN_FLIGHT keeps the second rule at every queue count.
 void defer_shape(const trt_ctx* c, uint32_t& group, uint32_t& slots) {
     const uint32_t T = std::max(c->defer_in_flight, 1u);
     if (c->frames_in_flight) {
@@ -760,6 +764,11 @@ void defer_shape(const trt_ctx* c, uint32_t& group, uint32_t& slots) {
     if (c->defer_group) {
         group = c->defer_group;
         slots = std::max(1u, (T + group - 1) / group);
+        return;
+    }
+    if (c->hw_queues >= 16u && !c->defer_in_flight_set) {
+        slots = 8u;
+        group = 3u;
         return;
     }
     slots = std::min(T, std::max(2u, c->hw_queues / 2u));
