@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--out", default="")
+    ap.add_argument("--records", type=int, default=0,
+                    help="workgroup records (default: one per tile; a deferred frame's pass A: tiles x defer_sub)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -32,7 +34,7 @@ def main():
     p = sc.params()
     r = trt.Renderer(0)
     r.upload_scene(sc)
-    ntiles = ((p.width + 7) // 8) * ((p.height + 7) // 8)
+    ntiles = a.records or ((p.width + 7) // 8) * ((p.height + 7) // 8)
     out8 = torch.empty((p.height, p.width, 4), dtype=torch.uint8, device="cuda")
     rec = torch.zeros((p.height, p.width, 4), dtype=torch.float32, device="cuda")
     res = []

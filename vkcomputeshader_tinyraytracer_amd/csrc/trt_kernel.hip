@@ -2503,6 +2503,20 @@ __global__ __launch_bounds__(64, (trace_waves<GEOM, CAP, SPLIT, DEFER>())) void 
         }
         tile = xcd_tile(A, t / Sd);
         trace_tile<CAP, COUNT, GEOM, SPLIT, DEFER, HYB>(A, A.fr[f], tile, cnt, lds, slab, t % Sd, f);
+#ifdef TRT_DIAG_WAVE_CLOCK
+        // diagnostic: pass A's record per block of a single deferred frame in out32 (waveclock.py
+        // --records ntiles * defer_sub)
+        if (threadIdx.x == 0 && A.out32 && A.dframes <= 1u) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            uint32_t* rec = reinterpret_cast<uint32_t*>(A.out32) + 4 * (size_t)blockIdx.x;
+            uint32_t xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            rec[0] = tile | ((xcc & 15u) << 28);
+            rec[1] = (uint32_t)t_start;
+            rec[2] = (uint32_t)(t_end - t_start);
+            rec[3] = (uint32_t)(t_start >> 32);
+        }
+#endif
         return;
     } else {
         tile = xcd_tile(A, t);
