@@ -245,7 +245,7 @@ struct KArgs {
     uint2* __restrict__ px_ev;        // per output pixel: (root event slot or kEvNone, 0)
     uint32_t* __restrict__ fb;        // output pixels re-traced with in-place shadows
     DeferCtr* __restrict__ dctr;
-    uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4: trace_tile)
+    uint32_t defer_sub;               // pass A waves per 8x8 tile (1, 2, 4, 8: trace_tile)
     // frames of a deferred launch (trt_render_frames groups consecutive frames): frame f's
     // scratch is ev + f * ev_fstride, shq + f * shq_fstride, px_ev / fb + f * px_fstride, dctr + f
     uint32_t dframes;

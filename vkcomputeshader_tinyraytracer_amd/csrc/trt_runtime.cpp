@@ -221,9 +221,9 @@ int trt_create(trt_ctx** out, int hip_device) {
     }
     if (const char* e = std::getenv("TRT_BVH_WAVES4")) c->bvh_waves4 = std::atoi(e) != 0 ? 1 : 0;
     if (const char* e = std::getenv("TRT_SPP_LANES")) c->spp_lanes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32 or 16
+    if (const char* e = std::getenv("TRT_DEFER_PPW")) { // pass-A pixels per wave: 64, 32, 16 or 8
         const int ppw = std::atoi(e);
-        c->defer_sub = ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
+        c->defer_sub = ppw == 8 ? 8u : ppw == 16 ? 4u : ppw == 32 ? 2u : ppw == 64 ? 1u : 0u;
     }
     if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) c->hw_queues = (uint32_t)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("TRT_DEFER_INTER")) c->defer_inter = (uint32_t)std::min(2, std::max(0, std::atoi(e)));
@@ -780,7 +780,7 @@ void defer_shape(const trt_ctx* c, uint32_t& group, uint32_t& slots) {
 size_t defer_slot_bytes(const trt_ctx* c, const trt_params* p, uint32_t slot, uint32_t frames) {
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     const size_t ntiles = ((p->width + 7u) / 8u) * ((trt_output_rows(p) + 7u) / 8u);
-    const DeferSizes z = defer_sizes(ntiles, p->max_depth, npx);
+    const DeferSizes z = defer_sizes(ntiles * std::max(1u, c->defer_sub / 2u), p->max_depth, npx); // as prepare_defer
     return defer_bufs_fit(c->split[slot], z, npx, frames) ? 0 : z.bytes * frames;
 }
 
@@ -817,8 +817,17 @@ void free_defer_bufs(trt_ctx::SplitBufs& b) {
 int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     auto& b = c->split[slot];
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
-    const DeferSizes z = defer_sizes(A.ntiles, p->max_depth, npx);
     const uint32_t G = std::max(A.nframes, 1u); // frames of this launch, each with its own scratch
+    // pass-A waves per tile (pool design): explicit (TRT_DEFER_PPW), else by the frames that
+    // overlap: with few frames in flight a frame's latency — its deepest tile's chain of
+    // segments — sets the rate, and two waves per tile halve that chain (the shipped frame at 2
+    // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
+    // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
+    const uint32_t Sd = c->defer_sub ? c->defer_sub : (c->cur_in_flight * G <= 4u ? 2u : 1u);
+    // every pass-A wave takes its own event chunks (a row of 64 lanes per step, idle lanes'
+    // slots unused): four waves per tile need twice the chunks of two (the shipped frame at two
+    // waves peaks at 60 % of the capacity, profiles/r06z_defer_probe.jsonl)
+    const DeferSizes z = defer_sizes(A.ntiles * std::max(1u, Sd / 2u), p->max_depth, npx);
     if (!defer_bufs_fit(b, z, npx, G)) {
         free_defer_bufs(b);
         hipError_t e = hipSuccess;
@@ -841,12 +850,7 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
         b.dframes = G;
     }
     A.defer = 1;
-    // pass-A waves per tile (pool design): explicit (TRT_DEFER_PPW), else by the frames that
-    // overlap: with few frames in flight a frame's latency — its deepest tile's chain of
-    // segments — sets the rate, and two waves per tile halve that chain (the shipped frame at 2
-    // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
-    // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
-    A.defer_sub = c->defer_sub ? c->defer_sub : (c->cur_in_flight * G <= 4u ? 2u : 1u);
+    A.defer_sub = Sd;
     A.defer_inter = c->defer_inter;
     // test hooks: tiny capacities exercise the in-place fallback (tests/test_gpu_defer.py)
     A.ev_cap = (uint32_t)env_cap("TRT_DEFER_EVCAP", z.chunks / trt::kDeferStripes);
