@@ -819,11 +819,14 @@ int prepare_defer(trt_ctx* c, const trt_params* p, KArgs& A, uint32_t slot) {
     const size_t npx = (size_t)trt_output_rows(p) * p->width;
     const uint32_t G = std::max(A.nframes, 1u); // frames of this launch, each with its own scratch
     // pass-A waves per tile (pool design): explicit (TRT_DEFER_PPW), else by the frames that
-    // overlap: with few frames in flight a frame's latency — its deepest tile's chain of
-    // segments — sets the rate, and two waves per tile halve that chain (the shipped frame at 2
-    // in flight 1.09 -> 0.82 ms); with many, the idle lanes of the cheap tiles cost more than the
-    // overlap hides (at 16 in flight 0.32 -> 0.40 ms), profiles/r05j_ab_defer_ppw.jsonl
-    const uint32_t Sd = c->defer_sub ? c->defer_sub : (c->cur_in_flight * G <= 4u ? 2u : 1u);
+    // overlap: with few frames in flight a frame's latency — its deepest tiles' chains of walks —
+    // sets the rate, and more waves per tile spread a deep tile's pixels (the shipped frame at 2
+    // in flight: 1 wave 1.09, 2 waves 0.82 ms, profiles/r05j_ab_defer_ppw.jsonl; 4 waves a
+    // further -2 % on both deep scenes at 2 in flight, 8 waves +12 % / -10 %, and at 4 in flight
+    // 2 waves stay best, profiles/r06zb_ab_pass_a_waves_per_tile.jsonl); with many, the idle
+    // lanes of the cheap tiles cost more than the overlap hides (at 16 in flight 0.32 -> 0.40 ms)
+    const uint32_t ov = c->cur_in_flight * G;
+    const uint32_t Sd = c->defer_sub ? c->defer_sub : ov <= 2u ? 4u : ov <= 4u ? 2u : 1u;
     // every pass-A wave takes its own event chunks (a row of 64 lanes per step, idle lanes'
     // slots unused): four waves per tile need twice the chunks of two (the shipped frame at two
     // waves peaks at 60 % of the capacity, profiles/r06z_defer_probe.jsonl)
