@@ -213,11 +213,12 @@ def test_count_frames_keep_reference_counters(gpu_renderer, scenes):
         assert gst[k] == ost[k], k
 
 
-@pytest.mark.parametrize("ppw", ["16", "32", "64"])
+@pytest.mark.parametrize("ppw", ["8", "16", "32", "64"])
 def test_pass_a_pixels_per_wave(scenes, ppw):
-    """TRT_DEFER_PPW: pass A with 64 / 32 / 16 pixels per wave (1, 2, 4 waves per 8x8 tile, the
-    other lanes fed by the wave's segment pool) — the frame is the unsplit loop's bit for bit
-    (the automatic choice, 2 waves per tile at <= 4 frames in flight, is what trt_render runs)."""
+    """TRT_DEFER_PPW: pass A with 64 / 32 / 16 / 8 pixels per wave (1, 2, 4, 8 waves per 8x8
+    tile, the other lanes fed by the wave's segment pool) — the frame is the unsplit loop's bit
+    for bit (the automatic choice, 4 waves per tile at <= 2 frames in flight, is what trt_render
+    runs)."""
     import os
 
     import vkcomputeshader_tinyraytracer_amd as trt
