@@ -150,9 +150,10 @@ int trt_render(trt_ctx* ctx, const trt_params* p, uint8_t* out_rgba8, float* out
  * runs on in-flight slot i % n: slot 0 is the context's stream, slots 1..n-1 are streams the
  * context owns, forked from and joined back into its stream inside the call, so frame i+1's
  * workgroups fill the GPU while frame i's slowest tiles finish.  n in [1, 32], or 0 = auto
- * (the default): 4, or 16 for deferred-shadow frames, whose depth-20 trees leave the longest
- * tails (measured: profiles/r02_ab_queues_*.log; 16 vs 8 in round 4: the shipped frame -16 %,
- * the README scene -28 %, profiles/r04z_ab_deferred_in_flight.jsonl).  Each slot is a HIP stream, so the process
+ * (the default): 4, or for deferred-shadow frames, whose depth-20 trees leave the longest
+ * tails, a shape by the hardware queues (below; measured: profiles/r02_ab_queues_*.log,
+ * profiles/r04z_ab_deferred_in_flight.jsonl, profiles/r06t_ab_defer_shape_32q.jsonl).  With n
+ * set, deferred frames go one per launch on the n slots.  Each slot is a HIP stream, so the process
  * needs as many hardware queues: the library leaves GPU_MAX_HW_QUEUES to the host (HIP's
  * default is 4; the Python package and bench.py raise it to 32 before HIP initialises, see
  * INTEGRATION.md) and only reads it: with auto in-flight, a deferred loop runs slots tracing
